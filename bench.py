@@ -1,0 +1,235 @@
+"""Headline benchmark: agent-steps/s of the batched colony (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c3|c2]
+
+One "step" = one Delta t = 1 s of the whole colony: every agent's kinetics
+(adaptive DP5(4), FP64, rtol 1e-8 / atol 1e-12), the local-environment
+gather, 100 diffusion substeps of every lattice field, and the agent-ordered
+exchange scatter.  Default workload = BASELINE config 4 (1M agents on a
+4096 x 4096 lattice, glucose + acetate), strong-scaled over N ranks by row
+bands (one process per GPU, RCCL halo exchange).  Inputs are resident in
+HBM before the timed region.  Rank 0 prints one JSON line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from lens_amd import configs  # noqa: E402
+from lens_amd.colony import Colony  # noqa: E402
+from lens_amd.lattice import Lattice, n_substeps  # noqa: E402
+from lens_amd.rate_law_compiler import compile_rate_laws  # noqa: E402
+
+METRIC = 'agent-steps/sec (whole node) at 1M agents; FP64 % peak; stencil HBM GB/s'
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: 8 TB/s spec
+FP64_PEAK_TFLOPS = 78.6         # 256 CU x 4 SIMD x 16 lanes x 2 x 2.4 GHz (vector FP64, spec)
+
+WORKLOADS = {
+    # name: (agents, lattice n, bounds um, description)
+    'c4': (1_000_000, 4096, 4096.0, 'BASELINE config 4: 1M agents + 4096x4096 diffusion_field lattice'),
+    'c3': (100_000, 1024, 1024.0, 'BASELINE config 3: 100k agents + 1024x1024 diffusion_field lattice'),
+    'c2': (10_000, 0, 0.0, 'BASELINE config 2: 10k heterogeneous agents, no lattice'),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--warmup', type=int, default=3)
+    p.add_argument('--workload', default='c4', choices=sorted(WORKLOADS))
+    p.add_argument('--integrator', default='dopri5', choices=['dopri5', 'euler'])
+    p.add_argument('--halo', type=int, default=10, help='halo depth = substeps per halo exchange')
+    p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
+    p.add_argument('--no-cpu-baseline', action='store_true')
+    p.add_argument('--cpu-seconds', type=float, default=12.0)
+    return p.parse_args()
+
+
+def build_rank(args, rank, world, dev):
+    n_total, nx, bound, _ = WORKLOADS[args.workload]
+    cfg = configs.glc_ac_config() if nx else configs.glc_lct_config()
+    table = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    rng = np.random.default_rng(configs.SEED + rank)
+    lat = None
+    if nx:
+        from lens_amd.distributed import row_bands
+        band = row_bands(nx, world)[rank]
+        n_local = n_total // world + (1 if rank < n_total % world else 0)
+        glc = configs.gaussian_bump_field((nx, nx))
+        lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (bound, bound), 10.0, 5.0, device=dev,
+                      row_band=band if world > 1 else None, halo=args.halo if world > 1 else 0,
+                      initial={'glc__D_e': glc, 'ac_e': np.zeros((nx, nx))})
+        x = rng.uniform(band[0] * bound / nx, band[1] * bound / nx, n_local)
+        y = rng.uniform(0.0, bound, n_local)
+        loc = np.stack([x, y])
+    else:
+        n_local = n_total // world + (1 if rank < n_total % world else 0)
+    params, conc = configs.heterogeneous_colony(table, cfg, n_local, seed=configs.SEED + rank)
+    col = Colony(cfg, n_local, device=dev, integrator=args.integrator, environment=lat or 'held',
+                 table=table, exchange=args.exchange)
+    col.set_agents(params=params, conc=conc, location=loc if nx else None)
+    if nx:
+        col.gather_external()
+    return col, lat, (params, conc, loc if nx else None)
+
+
+def cpu_baseline(args, col, host_state):
+    """The oracle's C restatement (OpenMP) on this host, on a bounded sample of
+    the same workload: whole steps, repeated until ~cpu_seconds have passed."""
+    from oracle import cpu
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+    os.environ.setdefault('OMP_NUM_THREADS', str(threads))
+    cpu.build()
+    params, conc, loc = host_state
+    conc = conc.copy()
+    t = col.table
+    desc = cpu.Desc(t)
+    n = conc.shape[1]
+    m2c = col.m2c[:n].cpu().numpy().copy()
+    h = np.zeros(n)
+    lat = col.lattice
+    fields = None
+    if lat is not None:
+        nx = lat.n_bins[0]
+        fields = [np.ascontiguousarray(configs.gaussian_bump_field((nx, nx))), np.zeros((nx, nx))]
+        coef = lat.diffusion * 0.01
+        n_sub = n_substeps(1.0)
+        bin_lin = col.bin_lin[:n].cpu().numpy().astype(np.int32)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        _, counts, _, _ = cpu.step_dopri5(desc, 1.0, params, conc, m2c, h_state=h,
+                                          rtol=col.rtol, atol=col.atol)
+        if fields is not None:
+            for f in fields:
+                cpu.diffuse(f, coef, n_sub)
+            for e, mol in enumerate(t.external_ids):
+                fi = lat.molecules.index(mol)
+                cpu.exchange(fields[fi].reshape(-1), bin_lin, counts[e], lat.binvol_avogadro)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= args.cpu_seconds or steps >= 20:
+            break
+    return {'value': steps * n / el, 'unit': 'agent-steps/s', 'cores': threads, 'kind': 'port',
+            'sample': '%d full step(s) of the same %d-agent workload (DP45 kinetics%s), %.1f s, '
+                      'oracle/cpu_kinetics.c with OpenMP' % (
+                          steps, n, ' + 100-substep stencil x %d fields + exchange' % len(fields)
+                          if fields is not None else '', el)}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+    col, lat, host_state = build_rank(args, rank, world, dev)
+    halo_ex = allred = None
+    if world > 1 and lat is not None:
+        from lens_amd.distributed import make_halo_exchange, make_minmax_allreduce
+        halo_ex = make_halo_exchange(lat, rank, world)
+        allred = make_minmax_allreduce()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        col.step(1.0, halo_exchange=halo_ex, allreduce=allred)
+    col.check_status()
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    timing = [{'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())}
+              for _ in range(args.steps)]
+    nsteps_acc = torch.zeros((), dtype=torch.int64, device=dev)
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing[k])
+        nsteps_acc += col.nsteps[:col.n].sum()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    col.check_status()
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    n_agents = torch.tensor([float(col.n)], dtype=torch.float64, device=dev)
+    kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
+    diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
+               if lat is not None else 0.0)
+    attempts = float(nsteps_acc.item())
+    if dist is not None:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(n_agents, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_agents = float(n_agents.item())
+    value = total_agents * args.steps / elapsed
+
+    if rank == 0:
+        n_total, nx, bound, desc = WORKLOADS[args.workload]
+        integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
+        integ = {'kernel': 'k_dopri5_thread', 'avg_ms_per_step': kin_ms,
+                 'dp45_attempts_per_agent_step': attempts / args.steps / col.n,
+                 'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),
+                 'achieved_tflops': integ_flops / (kin_ms * 1e-3) / 1e12 if kin_ms else None,
+                 'peak_tflops': FP64_PEAK_TFLOPS}
+        if integ['achieved_tflops'] is not None:
+            integ['frac'] = integ['achieved_tflops'] / FP64_PEAK_TFLOPS
+        roofline = None
+        if lat is not None:
+            n_sub = n_substeps(1.0)
+            rows = lat.rows_local
+            cells = (lat.row_hi - lat.row_lo) * lat.ny * len(lat.molecules)
+            bytes_per_launch = 16.0 * cells
+            launch_ms = diff_ms / n_sub
+            achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+            traffic = None
+            pmc = os.path.join(REPO, 'profiles', 'pmc_diffuse.json')
+            if os.path.exists(pmc) and world == 1:
+                with open(pmc) as f:
+                    traffic = json.load(f).get('hbm_bytes_per_launch')
+            roofline = {'bound': 'hbm', 'kernel': 'k_diffuse_substep', 'achieved': achieved,
+                        'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
+                        'traffic': traffic, 'bytes_per_launch': bytes_per_launch,
+                        'avg_launch_ms': launch_ms}
+        else:
+            roofline = {'bound': 'fp64-valu', 'kernel': 'k_dopri5_thread',
+                        'achieved': integ.get('achieved_tflops'), 'peak': FP64_PEAK_TFLOPS,
+                        'unit': 'TFLOP/s', 'frac': integ.get('frac'), 'traffic': None}
+        out = {
+            'metric': METRIC, 'value': value, 'unit': 'agent-steps/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
+            'data': 'synthetic (seeded heterogeneous colony, SURVEY.md §8d distributions)',
+            'config': {'workload': desc, 'agents': n_total, 'lattice': [nx, nx] if nx else None,
+                       'fields': lat.molecules if lat is not None else None, 'dt_s': 1.0,
+                       'substeps_per_step': n_substeps(1.0) if nx else 0,
+                       'integrator': args.integrator, 'rtol': col.rtol, 'atol': col.atol,
+                       'exchange': args.exchange, 'parallelism': 'row-bands x%d' % world,
+                       'halo': args.halo if world > 1 else 0},
+            'roofline': roofline,
+            'integrator': integ,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out['cpu_baseline'] = cpu_baseline(args, col, host_state)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

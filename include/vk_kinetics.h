@@ -1,0 +1,199 @@
+/*
+ * vk_kinetics.h -- C ABI of the MI355X batched agent-kinetics engine.
+ *
+ * Drop-in boundary for the per-agent hot path of CovertLab/Lens ("vivarium").
+ * The reference has no native FFI for this path: it is pure Python calling
+ * numpy/scipy.  Each entry point below replaces one reference call site; the
+ * Python host layer (lens_amd/native.py via ctypes) is the only caller.  See
+ * INTEGRATION.md for the binding a vivarium maintainer would add.
+ *
+ *   vk_table_create / vk_table_destroy
+ *       replaces KineticFluxModel.__init__ -> make_configuration /
+ *       make_rate_laws (vivarium/library/kinetic_rate_laws.py:262-275,
+ *       :43-98, :183-237).  The host compiler (lens_amd/rate_law_compiler.py)
+ *       flattens the closures into the index arrays of vk_table_desc.
+ *   vk_rate_fluxes
+ *       replaces KineticFluxModel.get_fluxes (kinetic_rate_laws.py:277-297).
+ *   vk_step_euler
+ *       replaces ConvenienceKinetics.next_update
+ *       (vivarium/processes/convenience_kinetics.py:303-352): one forward-Euler
+ *       step, integer exchange counts truncated toward zero (:331).
+ *   vk_step_dopri5
+ *       replaces the reference's scipy.integrate.odeint step
+ *       (vivarium/processes/Kremling2007_transport.py:384) for convenience
+ *       networks: adaptive Dormand-Prince 5(4) over [0, dt] on the augmented
+ *       system (internal species + per-reaction flux integrals).
+ *   vk_field_minmax + vk_diffuse
+ *       replace DiffusionField.diffuse / diffusion_delta
+ *       (vivarium/processes/diffusion_field.py:385-407): fixed dt=0.01
+ *       substeps of the reflect-boundary 5-point Laplacian, uniform-field skip.
+ *   vk_gather
+ *       replaces DiffusionField.get_local_environments (:362-379).
+ *   vk_exchange_sorted / vk_exchange_atomic
+ *       replace update_field_with_exchange (vivarium/core/registry.py:149-183)
+ *       applied once per agent by Store.apply_update.
+ *   vk_bin_sites
+ *       replaces get_bin_site (vivarium/library/lattice_utils.py:18-40).
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers except vk_table_desc's, which are
+ *     host pointers copied at vk_table_create.  The library never frees caller
+ *     memory; vk_table is the only object it owns.
+ *   - Agent arrays are structure-of-arrays with row stride `ld` (>= n_agents):
+ *     element (row, agent) lives at [row * ld + agent].
+ *   - Every call is asynchronous on `stream` (a hipStream_t; NULL = legacy
+ *     default stream) and returns a vk_status.  Per-agent problems are
+ *     reported in the caller's int32 status[] array (vk_agent_status bits).
+ *   - All arithmetic is FP64.
+ */
+#ifndef VK_KINETICS_H
+#define VK_KINETICS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VK_ABI_VERSION 1
+
+typedef void *vk_stream_t;        /* hipStream_t */
+typedef struct vk_table vk_table; /* opaque, device-resident reaction table */
+
+enum vk_status {
+    VK_OK = 0,
+    VK_ERR_ARG = 1,   /* bad argument (null pointer, negative size, ...) */
+    VK_ERR_HIP = 2,   /* a HIP runtime call failed; see vk_last_error() */
+    VK_ERR_LIMIT = 3, /* network too large for the requested kernel variant */
+    VK_ERR_NOMEM = 4
+};
+
+enum vk_agent_status {
+    VK_AGENT_OK = 0,
+    VK_AGENT_MAX_STEPS = 1,   /* integrator hit max_steps before t = dt */
+    VK_AGENT_H_UNDERFLOW = 2, /* step size fell below 1e-14 * dt */
+    VK_AGENT_NONFINITE = 4    /* NaN/Inf in the state or an exchange count */
+};
+
+/* Flattened rate-law table (lens_amd/rate_law_compiler.py:RateLawTable). */
+typedef struct vk_table_desc {
+    int32_t n_species;   /* rows of the agent concentration array            */
+    int32_t n_dyn;       /* rows [0, n_dyn) receive deltas (non-external)    */
+    int32_t n_reactions; /* flux rows                                        */
+    int32_t n_rate_laws; /* (reaction, enzyme) closures, get_fluxes order    */
+    int32_t n_params;    /* per-agent parameter rows (kcat, Km)              */
+    int32_t n_ext;       /* exchange-count rows (external molecules)         */
+    int32_t n_sets;      /* cofactor / partition sets                        */
+    int32_t n_members;   /* (species, Km slot) members of all sets           */
+    int32_t n_upd;       /* stoichiometry entries of dyn species             */
+    int32_t n_exch;      /* stoichiometry entries of external molecules      */
+    const int32_t *rl_reaction; /* [n_rate_laws] reaction row               */
+    const int32_t *rl_enzyme;   /* [n_rate_laws] species row of the enzyme  */
+    const int32_t *rl_kcat;     /* [n_rate_laws] parameter row of kcat_f    */
+    const int32_t *rl_num_ptr;  /* [n_rate_laws+1] numerator sets           */
+    const int32_t *rl_den_ptr;  /* [n_rate_laws+1] partition sets           */
+    const int32_t *set_ptr;     /* [n_sets+1] members                       */
+    const int32_t *mem_species; /* [n_members] species row                  */
+    const int32_t *mem_param;   /* [n_members] parameter row of the Km      */
+    const int32_t *upd_ptr;     /* [n_dyn+1]                                */
+    const int32_t *upd_rxn;     /* [n_upd]                                  */
+    const double *upd_coeff;    /* [n_upd]                                  */
+    const int32_t *ex_ptr;      /* [n_ext+1]                                */
+    const int32_t *ex_rxn;      /* [n_exch]                                 */
+    const double *ex_coeff;     /* [n_exch]                                 */
+} vk_table_desc;
+
+typedef struct vk_ode_opts {
+    double rtol;       /* relative tolerance (scipy RK45 semantics)          */
+    double atol;       /* absolute tolerance                                 */
+    int32_t max_steps; /* attempted steps per agent per call                 */
+    int32_t variant;   /* 0 = agent-per-thread                               */
+} vk_ode_opts;
+
+int vk_abi_version(void);
+const char *vk_last_error(void);
+
+int vk_table_create(const vk_table_desc *desc, vk_table **out);
+int vk_table_destroy(vk_table *table);
+
+/* flux[r*ld + a] = sum over the reaction's rate laws (exact reference order). */
+int vk_rate_fluxes(const vk_table *t, int64_t n_agents, int64_t ld,
+                   const double *params, const double *conc, double *flux,
+                   vk_stream_t stream);
+
+/* One reference Euler step.  If delta is NULL, conc rows [0, n_dyn) are
+ * updated in place (conc += delta, the accumulate updater); otherwise conc is
+ * left untouched and delta[s*ld+a] receives the reference's update value
+ * (0 + sum_j (coeff_j*flux)*dt).  flux[r*ld+a] (set);
+ * counts[e*ld+a] = sum_j trunc(((coeff_j*flux)*dt)*m2c[a]).               */
+int vk_step_euler(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
+                  const double *params, double *conc, const double *mmol_to_counts,
+                  double *delta, double *flux, int64_t *counts, int32_t *status,
+                  vk_stream_t stream);
+
+/* Adaptive Dormand-Prince 5(4) over [0, dt].  External/enzyme rows are held.
+ * delta as for vk_step_euler (NULL: integrate conc in place; else
+ * delta = y(dt) - y(0), conc untouched).  h_state[a]: step-size carry-over
+ * (in/out; <= 0 selects the initial step).  flux = integral(flux)/dt;
+ * counts from the integral; nsteps = attempted steps.                     */
+int vk_step_dopri5(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
+                   const vk_ode_opts *opts, const double *params, double *conc,
+                   const double *mmol_to_counts, double *delta, double *h_state,
+                   double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
+                   vk_stream_t stream);
+
+/* Lattice fields: n_fields planes of rows x ny doubles, plane stride
+ * field_stride.  Local rows may include halo rows of neighbouring ranks.   */
+
+/* minmax[2f] = min, minmax[2f+1] = max over rows [row_lo, row_hi). */
+int vk_field_minmax(const double *fields, int32_t n_fields, int64_t field_stride,
+                    int32_t ny, int32_t row_lo, int32_t row_hi, double *minmax,
+                    vk_stream_t stream);
+
+/* Substeps [sub_begin, sub_begin+sub_count) of an n_sub-substep diffusion.
+ * Substep j reads src(j) and writes dst(j):
+ *   src(0) = field, src(j) = work[(j-1)&1]; dst(j) = work[j&1] except the
+ *   last substep, which writes field = field + (new - field).
+ * Owned rows are [row_lo, row_hi).  Within the call, substep j computes rows
+ * [max(lo_min, row_lo-g), min(hi_max, row_hi+g)) with
+ * g = sub_begin+sub_count-1-j (halo shrinking); rows lo_min and hi_max-1 are
+ * reflected (Neumann) if they are global edges (edge_top/edge_bot != 0).
+ * coeff_dt = (D/(dx*dy)) * 0.01.  minmax (nullable) skips uniform fields.  */
+int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
+               int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi,
+               int32_t lo_min, int32_t hi_max, int32_t edge_top, int32_t edge_bot,
+               int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
+               const double *minmax, vk_stream_t stream);
+
+/* dst[map_row[i]*ld + a] = fields[map_field[i]*field_stride + bin_lin[a]]. */
+int vk_gather(const double *fields, int64_t field_stride, const int32_t *bin_lin,
+              int64_t n_agents, const int32_t *map_field, const int32_t *map_row,
+              int32_t n_map, double *dst, int64_t ld, vk_stream_t stream);
+
+/* Deterministic exchange: for each occupied bin occ_bin[b] and each map entry
+ * i, field += counts[map_count[i]*ld + a] / binvol_avogadro * 1000 for its
+ * agents occ_agent[occ_ptr[b]..occ_ptr[b+1]) in that (agent) order --
+ * bit-identical to applying update_field_with_exchange agent by agent.   */
+int vk_exchange_sorted(double *fields, int64_t field_stride, const int32_t *occ_bin,
+                       const int32_t *occ_ptr, const int32_t *occ_agent, int32_t n_occ,
+                       const int64_t *counts, int64_t ld, const int32_t *map_count,
+                       const int32_t *map_field, int32_t n_map, double binvol_avogadro,
+                       vk_stream_t stream);
+
+/* Order-free exchange with float64 atomics (same sum, any order). */
+int vk_exchange_atomic(double *fields, int64_t field_stride, const int32_t *bin_lin,
+                       int64_t n_agents, const int64_t *counts, int64_t ld,
+                       const int32_t *map_count, const int32_t *map_field, int32_t n_map,
+                       double binvol_avogadro, vk_stream_t stream);
+
+/* bin = floor(loc*n/bound) mod n per axis; bin_lin = (ix - row_offset)*ny + iy.
+ * loc is [2][ld] (x row then y row).  ix_out (nullable) receives ix.     */
+int vk_bin_sites(const double *loc, int64_t n_agents, int64_t ld, int32_t nx, int32_t ny,
+                 double bound_x, double bound_y, int32_t row_offset, int32_t *bin_lin,
+                 int32_t *ix_out, vk_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* VK_KINETICS_H */

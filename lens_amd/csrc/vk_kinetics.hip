@@ -1,0 +1,613 @@
+// Batched convenience kinetics on MI355X (gfx950): rate-law table, reference
+// Euler step and adaptive Dormand-Prince 5(4), one agent per lane.
+//
+// Reference semantics: vivarium/library/kinetic_rate_laws.py:149-178 (rate
+// law), :277-297 (get_fluxes); vivarium/processes/convenience_kinetics.py:
+// 303-352 (Euler step + integer exchange counts).  Compiled with
+// -ffp-contract=off: the exact kernels reproduce the reference's Python
+// floating-point operation order bit for bit; the DP45 kernel uses explicit
+// fma() where it wants one.
+//
+// Layout: agent state is SoA, row stride ld, so lane a of a wave touches
+// consecutive addresses for every row (coalesced 8-B-per-lane accesses).
+// The table is identical for every lane, so its walk is wave-uniform and is
+// read through the scalar cache (ldc()) -- no VGPRs, no LDS traffic.
+// The ODE kernel keeps each lane's species vector as a column of an LDS
+// tile (row s at lds[s*BS + lane]) because the rate laws index species at
+// run time; the integrator's stage vectors stay in VGPRs (static indices).
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "vk_internal.h"
+
+namespace vk {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+int hip_check(hipError_t e, const char *what) {
+    if (e == hipSuccess) return VK_OK;
+    set_error("%s: %s", what, hipGetErrorString(e));
+    return VK_ERR_HIP;
+}
+
+int launch_check(const char *what) { return hip_check(hipGetLastError(), what); }
+
+}  // namespace vk
+
+extern "C" int vk_abi_version(void) { return VK_ABI_VERSION; }
+extern "C" const char *vk_last_error(void) { return vk::g_err; }
+
+// ---------------------------------------------------------------------------
+// table management
+// ---------------------------------------------------------------------------
+
+extern "C" int vk_table_create(const vk_table_desc *d, vk_table **out) {
+    if (!d || !out) {
+        vk::set_error("vk_table_create: null argument");
+        return VK_ERR_ARG;
+    }
+    *out = nullptr;
+    if (d->n_species < 0 || d->n_dyn < 0 || d->n_dyn > d->n_species || d->n_reactions < 0 ||
+        d->n_rate_laws < 0 || d->n_params < 0 || d->n_ext < 0 || d->n_sets < 0 ||
+        d->n_members < 0 || d->n_upd < 0 || d->n_exch < 0) {
+        vk::set_error("vk_table_create: negative or inconsistent sizes");
+        return VK_ERR_ARG;
+    }
+    // validate every index on the host: a bad table must never reach a kernel
+    auto bad = [&](const char *what) {
+        vk::set_error("vk_table_create: invalid %s", what);
+        return VK_ERR_ARG;
+    };
+    const int L = d->n_rate_laws;
+    for (int l = 0; l < L; ++l) {
+        if (d->rl_reaction[l] < 0 || d->rl_reaction[l] >= d->n_reactions) return bad("rl_reaction");
+        if (d->rl_enzyme[l] < 0 || d->rl_enzyme[l] >= d->n_species) return bad("rl_enzyme");
+        if (d->rl_kcat[l] < 0 || d->rl_kcat[l] >= d->n_params) return bad("rl_kcat");
+    }
+    for (int l = 0; l <= L; ++l) {
+        if (d->rl_num_ptr[l] < 0 || d->rl_num_ptr[l] > d->n_sets) return bad("rl_num_ptr");
+        if (d->rl_den_ptr[l] < 0 || d->rl_den_ptr[l] > d->n_sets) return bad("rl_den_ptr");
+        if (l && (d->rl_num_ptr[l] < d->rl_num_ptr[l - 1] || d->rl_den_ptr[l] < d->rl_den_ptr[l - 1]))
+            return bad("set pointers (not monotone)");
+    }
+    for (int s = 0; s <= d->n_sets; ++s) {
+        if (d->set_ptr[s] < 0 || d->set_ptr[s] > d->n_members) return bad("set_ptr");
+        if (s && d->set_ptr[s] < d->set_ptr[s - 1]) return bad("set_ptr (not monotone)");
+    }
+    for (int m = 0; m < d->n_members; ++m) {
+        if (d->mem_species[m] < 0 || d->mem_species[m] >= d->n_species) return bad("mem_species");
+        if (d->mem_param[m] < 0 || d->mem_param[m] >= d->n_params) return bad("mem_param");
+    }
+    for (int i = 0; i <= d->n_dyn; ++i)
+        if (d->upd_ptr[i] < 0 || d->upd_ptr[i] > d->n_upd || (i && d->upd_ptr[i] < d->upd_ptr[i - 1]))
+            return bad("upd_ptr");
+    for (int j = 0; j < d->n_upd; ++j)
+        if (d->upd_rxn[j] < 0 || d->upd_rxn[j] >= d->n_reactions) return bad("upd_rxn");
+    for (int i = 0; i <= d->n_ext; ++i)
+        if (d->ex_ptr[i] < 0 || d->ex_ptr[i] > d->n_exch || (i && d->ex_ptr[i] < d->ex_ptr[i - 1]))
+            return bad("ex_ptr");
+    for (int j = 0; j < d->n_exch; ++j)
+        if (d->ex_rxn[j] < 0 || d->ex_rxn[j] >= d->n_reactions) return bad("ex_rxn");
+
+    // one blob: doubles first (8-B aligned), then int32 arrays
+    std::vector<double> dbl;
+    dbl.insert(dbl.end(), d->upd_coeff, d->upd_coeff + d->n_upd);
+    dbl.insert(dbl.end(), d->ex_coeff, d->ex_coeff + d->n_exch);
+    std::vector<int32_t> ints;
+    struct Seg { const int32_t *src; size_t n; size_t off; };
+    Seg segs[] = {
+        {d->rl_reaction, (size_t)L, 0}, {d->rl_enzyme, (size_t)L, 0}, {d->rl_kcat, (size_t)L, 0},
+        {d->rl_num_ptr, (size_t)L + 1, 0}, {d->rl_den_ptr, (size_t)L + 1, 0},
+        {d->set_ptr, (size_t)d->n_sets + 1, 0}, {d->mem_species, (size_t)d->n_members, 0},
+        {d->mem_param, (size_t)d->n_members, 0}, {d->upd_ptr, (size_t)d->n_dyn + 1, 0},
+        {d->upd_rxn, (size_t)d->n_upd, 0}, {d->ex_ptr, (size_t)d->n_ext + 1, 0},
+        {d->ex_rxn, (size_t)d->n_exch, 0},
+    };
+    for (auto &s : segs) {
+        s.off = ints.size();
+        ints.insert(ints.end(), s.src, s.src + s.n);
+    }
+    size_t dbytes = dbl.size() * sizeof(double);
+    size_t bytes = dbytes + ints.size() * sizeof(int32_t) + 16;
+    void *blob = nullptr;
+    int rc = vk::hip_check(hipMalloc(&blob, bytes), "hipMalloc(table)");
+    if (rc) return rc;
+    if (!dbl.empty()) {
+        rc = vk::hip_check(hipMemcpy(blob, dbl.data(), dbytes, hipMemcpyHostToDevice), "hipMemcpy(table)");
+        if (rc) { (void)hipFree(blob); return rc; }
+    }
+    int32_t *ibase = (int32_t *)((char *)blob + dbytes);
+    if (!ints.empty()) {
+        rc = vk::hip_check(hipMemcpy(ibase, ints.data(), ints.size() * sizeof(int32_t),
+                                     hipMemcpyHostToDevice), "hipMemcpy(table)");
+        if (rc) { (void)hipFree(blob); return rc; }
+    }
+    vk_table *t = new vk_table();
+    t->blob = blob;
+    t->n_sets = d->n_sets; t->n_members = d->n_members; t->n_upd = d->n_upd; t->n_exch = d->n_exch;
+    vk_dev_table &v = t->dev;
+    v.ib = ibase;
+    v.db = (const double *)blob;
+    v.n_species = d->n_species; v.n_dyn = d->n_dyn; v.n_reactions = d->n_reactions;
+    v.n_rate_laws = L; v.n_params = d->n_params; v.n_ext = d->n_ext;
+    v.o_upd_coeff = 0;
+    v.o_ex_coeff = d->n_upd;
+    v.o_rl_reaction = (int32_t)segs[0].off; v.o_rl_enzyme = (int32_t)segs[1].off;
+    v.o_rl_kcat = (int32_t)segs[2].off; v.o_rl_num_ptr = (int32_t)segs[3].off;
+    v.o_rl_den_ptr = (int32_t)segs[4].off; v.o_set_ptr = (int32_t)segs[5].off;
+    v.o_mem_species = (int32_t)segs[6].off; v.o_mem_param = (int32_t)segs[7].off;
+    v.o_upd_ptr = (int32_t)segs[8].off; v.o_upd_rxn = (int32_t)segs[9].off;
+    v.o_ex_ptr = (int32_t)segs[10].off; v.o_ex_rxn = (int32_t)segs[11].off;
+    *out = t;
+    return VK_OK;
+}
+
+extern "C" int vk_table_destroy(vk_table *t) {
+    if (!t) return VK_OK;
+    int rc = vk::hip_check(hipFree(t->blob), "hipFree(table)");
+    delete t;
+    return rc;
+}
+
+// ---------------------------------------------------------------------------
+// exact (reference-order) rate law, species/params read from global SoA
+// ---------------------------------------------------------------------------
+
+// cofactor_numerator / cofactor_denominator (kinetic_rate_laws.py:100-104):
+// a falsy Km (0, -0) gives 0 in the numerator and 1 in the denominator.
+__device__ __forceinline__ double rate_law_exact(const vk_dev_table &t, int l,
+                                                 const double *__restrict__ params,
+                                                 const double *__restrict__ conc, int64_t ld,
+                                                 int64_t a) {
+    double num = 0.0;
+    const int ns0 = TI(t, rl_num_ptr, l), ns1 = TI(t, rl_num_ptr, l + 1);
+    for (int s = ns0; s < ns1; ++s) {
+        double term = 1.0;
+        const int m0 = TI(t, set_ptr, s), m1 = TI(t, set_ptr, s + 1);
+        for (int m = m0; m < m1; ++m) {
+            const double km = params[(int64_t)TI(t, mem_param, m) * ld + a];
+            const double c = conc[(int64_t)TI(t, mem_species, m) * ld + a];
+            term = term * (km != 0.0 ? c / km : 0.0);
+        }
+        num = num + params[(int64_t)TI(t, rl_kcat, l) * ld + a] * term;
+    }
+    num = num * conc[(int64_t)TI(t, rl_enzyme, l) * ld + a];
+    double den = 1.0;
+    const int ds0 = TI(t, rl_den_ptr, l), ds1 = TI(t, rl_den_ptr, l + 1);
+    for (int s = ds0; s < ds1; ++s) {
+        double term = 1.0;
+        const int m0 = TI(t, set_ptr, s), m1 = TI(t, set_ptr, s + 1);
+        for (int m = m0; m < m1; ++m) {
+            const double km = params[(int64_t)TI(t, mem_param, m) * ld + a];
+            const double c = conc[(int64_t)TI(t, mem_species, m) * ld + a];
+            term = term * (km != 0.0 ? 1.0 + c / km : 1.0);
+        }
+        den = den + (term - 1.0);
+    }
+    return num / den;
+}
+
+__device__ __forceinline__ void fluxes_exact(const vk_dev_table &t, const double *__restrict__ params,
+                                             const double *__restrict__ conc, double *__restrict__ flux,
+                                             int64_t ld, int64_t a) {
+    for (int r = 0; r < t.n_reactions; ++r) flux[(int64_t)r * ld + a] = 0.0;
+    for (int l = 0; l < t.n_rate_laws; ++l) {
+        const double v = rate_law_exact(t, l, params, conc, ld, a);
+        const int64_t idx = (int64_t)TI(t, rl_reaction, l) * ld + a;
+        flux[idx] = flux[idx] + v;
+    }
+}
+
+// Python int(x) truncates toward zero; out-of-range / non-finite -> flagged.
+__device__ __forceinline__ int64_t trunc_count(double x, int32_t &st) {
+    if (!(fabs(x) < 9.2e18)) {
+        st |= VK_AGENT_NONFINITE;
+        return 0;
+    }
+    return (int64_t)x;
+}
+
+__global__ __launch_bounds__(256) void k_rate_fluxes(vk_dev_table t, int64_t n, int64_t ld,
+                                                     const double *__restrict__ params,
+                                                     const double *__restrict__ conc,
+                                                     double *__restrict__ flux) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= n) return;
+    fluxes_exact(t, params, conc, flux, ld, a);
+}
+
+// ConvenienceKinetics.next_update (convenience_kinetics.py:320-349) + the
+// accumulate updater: conc_s += (0 + sum_j (coeff_j*flux)*dt), counts_e =
+// sum_j int(((coeff_j*flux)*dt)*m2c).
+__global__ __launch_bounds__(256) void k_step_euler(vk_dev_table t, int64_t n, int64_t ld, double dt,
+                                                    const double *__restrict__ params,
+                                                    double *__restrict__ conc,
+                                                    const double *__restrict__ m2c,
+                                                    double *__restrict__ delta,
+                                                    double *__restrict__ flux,
+                                                    int64_t *__restrict__ counts,
+                                                    int32_t *__restrict__ status) {
+    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= n) return;
+    fluxes_exact(t, params, conc, flux, ld, a);
+    int32_t st = 0;
+    for (int s = 0; s < t.n_dyn; ++s) {
+        double d = 0.0;
+        const int j0 = TI(t, upd_ptr, s), j1 = TI(t, upd_ptr, s + 1);
+        for (int j = j0; j < j1; ++j)
+            d = d + (TD(t, upd_coeff, j) * flux[(int64_t)TI(t, upd_rxn, j) * ld + a]) * dt;
+        const int64_t idx = (int64_t)s * ld + a;
+        if (delta) {
+            if (!isfinite(d)) st |= VK_AGENT_NONFINITE;
+            delta[idx] = d;
+        } else {
+            const double v = conc[idx] + d;
+            if (!isfinite(v)) st |= VK_AGENT_NONFINITE;
+            conc[idx] = v;
+        }
+    }
+    const double mc = m2c[a];
+    for (int e = 0; e < t.n_ext; ++e) {
+        int64_t c = 0;
+        const int j0 = TI(t, ex_ptr, e), j1 = TI(t, ex_ptr, e + 1);
+        for (int j = j0; j < j1; ++j) {
+            const double sf = (TD(t, ex_coeff, j) * flux[(int64_t)TI(t, ex_rxn, j) * ld + a]) * dt;
+            c += trunc_count(sf * mc, st);
+        }
+        counts[(int64_t)e * ld + a] = c;
+    }
+    if (status) status[a] = st;
+}
+
+static int check_agents(const char *fn, const vk_table *t, int64_t n, int64_t ld) {
+    if (!t) {
+        vk::set_error("%s: null table", fn);
+        return VK_ERR_ARG;
+    }
+    if (n < 0 || ld < n) {
+        vk::set_error("%s: need 0 <= n_agents <= ld (n=%lld ld=%lld)", fn, (long long)n, (long long)ld);
+        return VK_ERR_ARG;
+    }
+    return VK_OK;
+}
+
+extern "C" int vk_rate_fluxes(const vk_table *t, int64_t n, int64_t ld, const double *params,
+                              const double *conc, double *flux, vk_stream_t stream) {
+    int rc = check_agents("vk_rate_fluxes", t, n, ld);
+    if (rc || n == 0) return rc;
+    if (!params || !conc || !flux) {
+        vk::set_error("vk_rate_fluxes: null array");
+        return VK_ERR_ARG;
+    }
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_rate_fluxes, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t->dev, n, ld,
+                       params, conc, flux);
+    return vk::launch_check("k_rate_fluxes");
+}
+
+extern "C" int vk_step_euler(const vk_table *t, int64_t n, int64_t ld, double dt, const double *params,
+                             double *conc, const double *m2c, double *delta, double *flux, int64_t *counts,
+                             int32_t *status, vk_stream_t stream) {
+    int rc = check_agents("vk_step_euler", t, n, ld);
+    if (rc || n == 0) return rc;
+    if (!params || !conc || !m2c || !flux || (!counts && t->dev.n_ext > 0)) {
+        vk::set_error("vk_step_euler: null array");
+        return VK_ERR_ARG;
+    }
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_step_euler, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t->dev, n, ld, dt,
+                       params, conc, m2c, delta, flux, counts, status);
+    return vk::launch_check("k_step_euler");
+}
+
+// ---------------------------------------------------------------------------
+// Dormand-Prince 5(4), agent per lane
+// ---------------------------------------------------------------------------
+//
+// y = [dyn species (n_dyn) | per-reaction flux integrals (n_reactions)], NY
+// entries, a compile-time constant so the seven stage vectors live in VGPRs.
+// LDS tile (BS lanes): rows [0,n_species) species, then n_reactions flux
+// rows, then n_params parameter rows holding kcat or 1/Km (0 for a falsy Km).
+
+namespace dp {
+constexpr double a21 = 1.0 / 5.0;
+constexpr double a31 = 3.0 / 40.0, a32 = 9.0 / 40.0;
+constexpr double a41 = 44.0 / 45.0, a42 = -56.0 / 15.0, a43 = 32.0 / 9.0;
+constexpr double a51 = 19372.0 / 6561.0, a52 = -25360.0 / 2187.0, a53 = 64448.0 / 6561.0,
+                 a54 = -212.0 / 729.0;
+constexpr double a61 = 9017.0 / 3168.0, a62 = -355.0 / 33.0, a63 = 46732.0 / 5247.0,
+                 a64 = 49.0 / 176.0, a65 = -5103.0 / 18656.0;
+constexpr double b1 = 35.0 / 384.0, b3 = 500.0 / 1113.0, b4 = 125.0 / 192.0,
+                 b5 = -2187.0 / 6784.0, b6 = 11.0 / 84.0;
+// e = b - bhat (4th-order embedded), scipy RK45's E up to sign
+constexpr double e1 = 71.0 / 57600.0, e3 = -71.0 / 16695.0, e4 = 71.0 / 1920.0,
+                 e5 = -17253.0 / 339200.0, e6 = 22.0 / 525.0, e7 = -1.0 / 40.0;
+constexpr double SAFETY = 0.9, MIN_FACTOR = 0.2, MAX_FACTOR = 10.0;
+}  // namespace dp
+
+constexpr int DP_BS = 256;
+
+// One rate law from the LDS tile (1/Km precomputed): num*E/den.
+__device__ __forceinline__ double rate_law_tile(const vk_dev_table &t, int l, const double *cl,
+                                                const double *pl, int lane) {
+    double num = 0.0;
+    const int ns0 = TI(t, rl_num_ptr, l), ns1 = TI(t, rl_num_ptr, l + 1);
+    for (int s = ns0; s < ns1; ++s) {
+        double term = pl[TI(t, rl_kcat, l) * DP_BS + lane];
+        const int m0 = TI(t, set_ptr, s), m1 = TI(t, set_ptr, s + 1);
+        for (int m = m0; m < m1; ++m)
+            term *= cl[TI(t, mem_species, m) * DP_BS + lane] * pl[TI(t, mem_param, m) * DP_BS + lane];
+        num += term;
+    }
+    num *= cl[TI(t, rl_enzyme, l) * DP_BS + lane];
+    double den = 1.0;
+    const int ds0 = TI(t, rl_den_ptr, l), ds1 = TI(t, rl_den_ptr, l + 1);
+    for (int s = ds0; s < ds1; ++s) {
+        double term = 1.0;
+        const int m0 = TI(t, set_ptr, s), m1 = TI(t, set_ptr, s + 1);
+        for (int m = m0; m < m1; ++m)
+            term *= fma(cl[TI(t, mem_species, m) * DP_BS + lane], pl[TI(t, mem_param, m) * DP_BS + lane], 1.0);
+        den += term - 1.0;
+    }
+    return num / den;
+}
+
+template <int NY>
+__device__ __forceinline__ void rhs_tile(const vk_dev_table &t, const double (&y)[NY], double (&dy)[NY],
+                                         double *cl, double *fl, const double *pl, int lane) {
+    const int nd = t.n_dyn;
+#pragma unroll
+    for (int i = 0; i < NY; ++i)
+        if (i < nd) cl[i * DP_BS + lane] = y[i];
+    for (int r = 0; r < t.n_reactions; ++r) fl[r * DP_BS + lane] = 0.0;
+    for (int l = 0; l < t.n_rate_laws; ++l) {
+        const double v = rate_law_tile(t, l, cl, pl, lane);
+        const int r = TI(t, rl_reaction, l);
+        fl[r * DP_BS + lane] += v;
+    }
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+        if (i < nd) {
+            double d = 0.0;
+            const int j0 = TI(t, upd_ptr, i), j1 = TI(t, upd_ptr, i + 1);
+            for (int j = j0; j < j1; ++j) d = fma(TD(t, upd_coeff, j), fl[TI(t, upd_rxn, j) * DP_BS + lane], d);
+            dy[i] = d;
+        } else if (i < nd + t.n_reactions) {
+            dy[i] = fl[(i - nd) * DP_BS + lane];
+        } else {
+            dy[i] = 0.0;   // padding of the NY bucket
+        }
+    }
+}
+
+// RMS over the ny live components (entries >= ny pad the NY bucket)
+template <int NY>
+__device__ __forceinline__ double rms_norm(const double (&v)[NY], const double (&scale)[NY], int ny) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+        if (i < ny) {
+            const double q = v[i] / scale[i];
+            s = fma(q, q, s);
+        }
+    }
+    return sqrt(s / ny);
+}
+
+template <int NY>
+__global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t n, int64_t ld, double dt,
+                                                         double rtol, double atol, int max_steps,
+                                                         const double *__restrict__ params,
+                                                         double *__restrict__ conc,
+                                                         const double *__restrict__ m2c,
+                                                         double *__restrict__ delta,
+                                                         double *__restrict__ h_state,
+                                                         double *__restrict__ flux,
+                                                         int64_t *__restrict__ counts,
+                                                         int32_t *__restrict__ status,
+                                                         int32_t *__restrict__ nsteps_out) {
+    extern __shared__ double lds[];
+    const int lane = threadIdx.x;
+    const int64_t a = (int64_t)blockIdx.x * DP_BS + lane;
+    double *cl = lds;                                 // [n_species][BS]
+    double *fl = lds + t.n_species * DP_BS;           // [n_reactions][BS]
+    double *pl = fl + t.n_reactions * DP_BS;          // [n_params][BS]
+    if (a >= n) return;                               // no block-wide sync below
+
+    // stage per-lane constants into the tile
+    for (int s = t.n_dyn; s < t.n_species; ++s) cl[s * DP_BS + lane] = conc[(int64_t)s * ld + a];
+    for (int p = 0; p < t.n_params; ++p) pl[p * DP_BS + lane] = params[(int64_t)p * ld + a];
+    for (int m = 0; m < TI(t, set_ptr, TI(t, rl_den_ptr, t.n_rate_laws)); ++m) {
+        const int p = TI(t, mem_param, m);
+        const double km = params[(int64_t)p * ld + a];
+        pl[p * DP_BS + lane] = (km != 0.0) ? 1.0 / km : 0.0;
+    }
+
+    const int nd = t.n_dyn;
+    const int ny = nd + t.n_reactions;
+    double y[NY], k1[NY], k2[NY], k3[NY], k4[NY], k5[NY], k6[NY], k7[NY], yt[NY];
+#pragma unroll
+    for (int i = 0; i < NY; ++i) y[i] = (i < nd) ? conc[(int64_t)i * ld + a] : 0.0;
+
+    rhs_tile<NY>(t, y, k1, cl, fl, pl, lane);
+    int32_t st = 0;
+    double h = h_state ? h_state[a] : 0.0;
+    if (!(h > 0.0)) {
+        // scipy select_initial_step (order 4)
+        double sc[NY];
+#pragma unroll
+        for (int i = 0; i < NY; ++i) sc[i] = fma(fabs(y[i]), rtol, atol);
+        const double d0 = rms_norm<NY>(y, sc, ny), d1 = rms_norm<NY>(k1, sc, ny);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = fmin(h0, dt);
+#pragma unroll
+        for (int i = 0; i < NY; ++i) yt[i] = fma(h0, k1[i], y[i]);
+        rhs_tile<NY>(t, yt, k2, cl, fl, pl, lane);
+#pragma unroll
+        for (int i = 0; i < NY; ++i) k2[i] = k2[i] - k1[i];
+        const double d2 = rms_norm<NY>(k2, sc, ny) / h0;
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3)
+                                                        : pow(0.01 / fmax(d1, d2), 0.2);
+        h = fmin(fmin(100.0 * h0, h1), dt);
+    }
+
+    double tt = 0.0;
+    int ns = 0;
+    bool rejected = false;
+    double h_keep = h;
+    while (tt < dt) {
+        if (ns >= max_steps) { st |= VK_AGENT_MAX_STEPS; break; }
+        if (h < 1e-14 * dt) { st |= VK_AGENT_H_UNDERFLOW; break; }
+        double hs = h;
+        bool last = false;
+        if (tt + hs >= dt) { hs = dt - tt; last = true; }
+        ++ns;
+#pragma unroll
+        for (int i = 0; i < NY; ++i) yt[i] = fma(hs, dp::a21 * k1[i], y[i]);
+        rhs_tile<NY>(t, yt, k2, cl, fl, pl, lane);
+#pragma unroll
+        for (int i = 0; i < NY; ++i) yt[i] = fma(hs, fma(dp::a32, k2[i], dp::a31 * k1[i]), y[i]);
+        rhs_tile<NY>(t, yt, k3, cl, fl, pl, lane);
+#pragma unroll
+        for (int i = 0; i < NY; ++i)
+            yt[i] = fma(hs, fma(dp::a43, k3[i], fma(dp::a42, k2[i], dp::a41 * k1[i])), y[i]);
+        rhs_tile<NY>(t, yt, k4, cl, fl, pl, lane);
+#pragma unroll
+        for (int i = 0; i < NY; ++i)
+            yt[i] = fma(hs, fma(dp::a54, k4[i], fma(dp::a53, k3[i], fma(dp::a52, k2[i], dp::a51 * k1[i]))), y[i]);
+        rhs_tile<NY>(t, yt, k5, cl, fl, pl, lane);
+#pragma unroll
+        for (int i = 0; i < NY; ++i)
+            yt[i] = fma(hs, fma(dp::a65, k5[i], fma(dp::a64, k4[i], fma(dp::a63, k3[i],
+                        fma(dp::a62, k2[i], dp::a61 * k1[i])))), y[i]);
+        rhs_tile<NY>(t, yt, k6, cl, fl, pl, lane);
+#pragma unroll
+        for (int i = 0; i < NY; ++i)
+            yt[i] = fma(hs, fma(dp::b6, k6[i], fma(dp::b5, k5[i], fma(dp::b4, k4[i],
+                        fma(dp::b3, k3[i], dp::b1 * k1[i])))), y[i]);
+        rhs_tile<NY>(t, yt, k7, cl, fl, pl, lane);
+        double en = 0.0;
+#pragma unroll
+        for (int i = 0; i < NY; ++i) {
+            if (i < ny) {
+                const double err = hs * fma(dp::e7, k7[i], fma(dp::e6, k6[i], fma(dp::e5, k5[i],
+                                       fma(dp::e4, k4[i], fma(dp::e3, k3[i], dp::e1 * k1[i])))));
+                const double q = err / fma(fmax(fabs(y[i]), fabs(yt[i])), rtol, atol);
+                en = fma(q, q, en);
+            }
+        }
+        en = sqrt(en / ny);
+        if (!isfinite(en)) { st |= VK_AGENT_NONFINITE; break; }
+        if (en < 1.0) {
+            double factor = (en == 0.0) ? dp::MAX_FACTOR : fmin(dp::MAX_FACTOR, dp::SAFETY * pow(en, -0.2));
+            if (rejected) factor = fmin(1.0, factor);
+            tt = last ? dt : tt + hs;
+#pragma unroll
+            for (int i = 0; i < NY; ++i) { y[i] = yt[i]; k1[i] = k7[i]; }
+            h_keep = last ? fmax(h, hs * factor) : hs * factor;
+            h = hs * factor;
+            rejected = false;
+        } else {
+            h = hs * fmax(dp::MIN_FACTOR, dp::SAFETY * pow(en, -0.2));
+            rejected = true;
+        }
+    }
+
+    // write back: species, mean fluxes, exchange counts from the integrals
+#pragma unroll
+    for (int i = 0; i < NY; ++i) {
+        if (i < nd) {
+            if (!isfinite(y[i])) st |= VK_AGENT_NONFINITE;
+            const int64_t idx = (int64_t)i * ld + a;
+            if (delta)
+                delta[idx] = y[i] - conc[idx];
+            else
+                conc[idx] = y[i];
+        } else if (i < ny) {
+            fl[(i - nd) * DP_BS + lane] = y[i];      // integrals back into the tile
+            flux[(int64_t)(i - nd) * ld + a] = y[i] / dt;
+        }
+    }
+    const double mc = m2c[a];
+    for (int e = 0; e < t.n_ext; ++e) {
+        int64_t c = 0;
+        const int j0 = TI(t, ex_ptr, e), j1 = TI(t, ex_ptr, e + 1);
+        for (int j = j0; j < j1; ++j)
+            c += trunc_count((TD(t, ex_coeff, j) * fl[TI(t, ex_rxn, j) * DP_BS + lane]) * mc, st);
+        counts[(int64_t)e * ld + a] = c;
+    }
+    if (h_state) h_state[a] = h_keep;
+    if (status) status[a] = st;
+    if (nsteps_out) nsteps_out[a] = ns;
+}
+
+template <int NY>
+static int launch_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,
+                         const double *params, double *conc, const double *m2c, double *delta, double *h_state,
+                         double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
+                         hipStream_t stream) {
+    const size_t lds = (size_t)(t->dev.n_species + t->dev.n_reactions + t->dev.n_params) * DP_BS * sizeof(double);
+    if (lds > 160 * 1024) {
+        vk::set_error("vk_step_dopri5: network needs %zu B of LDS per 256-agent tile (> 160 KiB); "
+                      "use the agent-per-wavefront variant", lds);
+        return VK_ERR_LIMIT;
+    }
+    static bool attr_set = false;
+    if (lds > 64 * 1024 && !attr_set) {
+        (void)hipFuncSetAttribute((const void *)k_dopri5_thread<NY>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_set = true;
+    }
+    const unsigned blocks = (unsigned)((n + DP_BS - 1) / DP_BS);
+    hipLaunchKernelGGL(k_dopri5_thread<NY>, dim3(blocks), dim3(DP_BS), lds, stream, t->dev, n, ld, dt, o->rtol,
+                       o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux, counts, status, nsteps);
+    return vk::launch_check("k_dopri5_thread");
+}
+
+extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,
+                              const double *params, double *conc, const double *m2c, double *delta, double *h_state,
+                              double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
+                              vk_stream_t stream) {
+    int rc = check_agents("vk_step_dopri5", t, n, ld);
+    if (rc || n == 0) return rc;
+    if (!o || !params || !conc || !m2c || !flux || (!counts && t->dev.n_ext > 0)) {
+        vk::set_error("vk_step_dopri5: null argument");
+        return VK_ERR_ARG;
+    }
+    if (!(dt > 0.0) || !(o->rtol > 0.0) || !(o->atol >= 0.0) || o->max_steps <= 0) {
+        vk::set_error("vk_step_dopri5: need dt > 0, rtol > 0, atol >= 0, max_steps > 0");
+        return VK_ERR_ARG;
+    }
+    if (o->variant != 0) {
+        vk::set_error("vk_step_dopri5: variant %d not available", o->variant);
+        return VK_ERR_ARG;
+    }
+    const int ny = t->dev.n_dyn + t->dev.n_reactions;
+    hipStream_t s = (hipStream_t)stream;
+#define VK_DP(NYC) return launch_dopri5<NYC>(t, n, ld, dt, o, params, conc, m2c, delta, h_state, flux, counts, status, nsteps, s)
+    switch (ny) {
+        case 1: VK_DP(1); case 2: VK_DP(2); case 3: VK_DP(3); case 4: VK_DP(4);
+        case 5: VK_DP(5); case 6: VK_DP(6); case 7: VK_DP(7); case 8: VK_DP(8);
+        case 9: VK_DP(9); case 10: VK_DP(10); case 11: VK_DP(11); case 12: VK_DP(12);
+        default: break;
+    }
+    if (ny <= 16) VK_DP(16);
+    if (ny <= 24) VK_DP(24);
+    if (ny <= 32) VK_DP(32);
+#undef VK_DP
+    vk::set_error("vk_step_dopri5: %d integrated components > 32 (agent-per-thread limit)", ny);
+    return VK_ERR_LIMIT;
+}

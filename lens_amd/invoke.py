@@ -1,0 +1,151 @@
+"""Batching ``invoke`` hook for the reference ``Experiment``.
+
+``Experiment`` calls ``self.invoke(process, interval, states)`` for every
+process that is due and consumes the result only through ``.get()`` inside
+``send_updates`` (vivarium/core/experiment.py:1157-1178, 1230, 1282-1311,
+1338-1341).  :class:`BatchedInvoke` exploits that: it records each
+``BatchedConvenienceKinetics`` call (packing the agent's state into a host
+SoA row immediately, since ``states`` are live store references), and the
+first ``.get()`` of the step launches ONE kernel per (network, interval)
+group for all recorded agents.  Other processes run immediately, as with the
+reference's ``InvokeProcess``.
+
+    experiment = Experiment({..., 'invoke': BatchedInvoke()})
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import numpy as np
+import torch
+
+from lens_amd.kinetics import KineticsEngine
+from lens_amd.process import BatchedConvenienceKinetics
+
+_ENGINES: Dict[Tuple[str, int], KineticsEngine] = {}
+
+
+def engine_for(process: BatchedConvenienceKinetics, device=None) -> KineticsEngine:
+    dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+    key = (process.signature, dev.index if dev.index is not None else 0)
+    eng = _ENGINES.get(key)
+    if eng is None:
+        eng = KineticsEngine(process.table, dev)
+        _ENGINES[key] = eng
+    return eng
+
+
+class _Packed:
+    __slots__ = ('process', 'interval', 'conc', 'm2c')
+
+    def __init__(self, process, interval, states):
+        self.process = process
+        self.interval = float(interval)
+        self.conc = np.zeros(process.table.n_species, dtype=np.float64)
+        self.m2c = process.pack_state(states, self.conc)
+
+
+def _run_group(items: List[_Packed], device=None) -> List[dict]:
+    p0 = items[0].process
+    t = p0.table
+    eng = engine_for(p0, device)
+    n = len(items)
+    dev = eng.device
+    conc = torch.from_numpy(np.stack([it.conc for it in items], axis=1)).to(dev).contiguous()
+    params = torch.from_numpy(np.stack([it.process.param_values for it in items], axis=1)).to(dev).contiguous()
+    m2c = torch.tensor([it.m2c for it in items], dtype=torch.float64, device=dev)
+    delta = torch.zeros((t.n_dyn, n), dtype=torch.float64, device=dev)
+    integrator = p0.parameters.get('integrator', 'euler')
+    dt = items[0].interval
+    if integrator == 'euler':
+        flux, counts, status = eng.euler(dt, params, conc, m2c, delta=delta)
+    elif integrator == 'dopri5':
+        h = torch.tensor([getattr(it.process, '_h_state', 0.0) for it in items],
+                         dtype=torch.float64, device=dev)
+        flux, counts, status, _ = eng.dopri5(
+            dt, params, conc, m2c, h_state=h, delta=delta,
+            rtol=p0.parameters.get('rtol', 1e-8), atol=p0.parameters.get('atol', 1e-12),
+            max_steps=p0.parameters.get('max_steps', 100000))
+        for it, hv in zip(items, h.cpu().numpy()):
+            it.process._h_state = float(hv)
+    else:
+        raise ValueError('unknown integrator %r' % integrator)
+    flux_h = flux.cpu().numpy()
+    delta_h = delta.cpu().numpy()
+    counts_h = counts.cpu().numpy()
+    st = status.cpu().numpy()
+    if st.any():
+        bad = int(np.flatnonzero(st)[0])
+        raise FloatingPointError('agent %d: kernel status %d (1=max steps, 2=step underflow, '
+                                 '4=non-finite)' % (bad, int(st[bad])))
+    return [it.process.unpack_update(flux_h[:, i], delta_h[:, i], counts_h[:, i])
+            for i, it in enumerate(items)]
+
+
+def run_batch(calls, device=None) -> List[dict]:
+    """Evaluate [(process, interval, states)] in as few launches as possible."""
+    packed = [_Packed(p, dt, s) for p, dt, s in calls]
+    groups: Dict[Tuple[str, float, str], List[int]] = {}
+    for i, it in enumerate(packed):
+        key = (it.process.signature, it.interval, it.process.parameters.get('integrator', 'euler'))
+        groups.setdefault(key, []).append(i)
+    out: List[dict] = [None] * len(packed)
+    for idx in groups.values():
+        res = _run_group([packed[i] for i in idx], device)
+        for i, r in zip(idx, res):
+            out[i] = r
+    return out
+
+
+class _Future:
+    def __init__(self, owner, slot):
+        self.owner = owner
+        self.slot = slot
+
+    def get(self, timeout=0):
+        return self.owner._result(self.slot)
+
+
+class _Immediate:
+    def __init__(self, update):
+        self.update = update
+
+    def get(self, timeout=0):
+        return self.update
+
+
+class BatchedInvoke:
+    """Drop-in value for ``Experiment(config['invoke'])``."""
+
+    def __init__(self, device=None):
+        self.device = device
+        self._pending = []
+        self._results = {}
+        self._next = 0
+
+    def __call__(self, process, interval, states):
+        if not isinstance(process, BatchedConvenienceKinetics):
+            return _Immediate(process.next_update(interval, states))
+        slot = self._next
+        self._next += 1
+        self._pending.append((slot, _Packed(process, interval, states)))
+        return _Future(self, slot)
+
+    def flush(self):
+        if not self._pending:
+            return
+        pending, self._pending = self._pending, []
+        groups: Dict[Tuple, List[Tuple[int, _Packed]]] = {}
+        for slot, it in pending:
+            key = (it.process.signature, it.interval, it.process.parameters.get('integrator', 'euler'))
+            groups.setdefault(key, []).append((slot, it))
+        for members in groups.values():
+            res = _run_group([it for _, it in members], self.device)
+            for (slot, _), r in zip(members, res):
+                self._results[slot] = r
+
+    def _result(self, slot):
+        if slot not in self._results:
+            self.flush()
+        return self._results.pop(slot)

@@ -1,0 +1,132 @@
+"""Device kinetics operators over SoA torch tensors (FP64, one agent per column).
+
+Thin, shape-checked wrappers over the C ABI.  Layout (``include/vk_kinetics.h``):
+``params[n_params, ld]``, ``conc[n_species, ld]``, ``mmol_to_counts[ld]``,
+``flux[n_reactions, ld]``, ``counts[n_ext, ld]`` (int64); agents are columns
+``0..n_agents-1``; rows follow :class:`~lens_amd.rate_law_compiler.RateLawTable`.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from lens_amd import native
+from lens_amd.rate_law_compiler import RateLawTable
+
+F64 = torch.float64
+
+
+def _need(t, name, rows, ld, dtype, device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError('%s must be a torch tensor' % name)
+    if t.dtype != dtype:
+        raise TypeError('%s must be %s, got %s' % (name, dtype, t.dtype))
+    if t.device.type != 'cuda' or (device is not None and t.device != device):
+        raise ValueError('%s must live on %s' % (name, device))
+    if not t.is_contiguous():
+        raise ValueError('%s must be contiguous' % name)
+    want = (rows, ld) if rows is not None else (ld,)
+    if tuple(t.shape) != want:
+        raise ValueError('%s has shape %s, kernel expects %s' % (name, tuple(t.shape), want))
+
+
+class KineticsEngine:
+    """A compiled network resident on one GPU."""
+
+    def __init__(self, table: RateLawTable, device=None):
+        self.table = table
+        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        with torch.cuda.device(self.device):
+            self.dev = native.DeviceTable(table)
+
+    # -- allocation helpers -------------------------------------------------
+    def empty_like_agents(self, rows, ld, dtype=F64):
+        shape = (rows, ld) if rows is not None else (ld,)
+        return torch.zeros(shape, dtype=dtype, device=self.device)
+
+    def _check_state(self, params, conc, n_agents):
+        t = self.table
+        ld = conc.shape[1]
+        if not (0 <= n_agents <= ld):
+            raise ValueError('n_agents must be in [0, ld]')
+        _need(params, 'params', t.n_params, ld, F64, self.device)
+        _need(conc, 'conc', t.n_species, ld, F64, self.device)
+        return ld
+
+    # -- operators ----------------------------------------------------------
+    def fluxes(self, params, conc, n_agents=None, flux=None):
+        n = conc.shape[1] if n_agents is None else n_agents
+        ld = self._check_state(params, conc, n)
+        if flux is None:
+            flux = self.empty_like_agents(self.table.n_reactions, ld)
+        _need(flux, 'flux', self.table.n_reactions, ld, F64, self.device)
+        native.check(native._lib.vk_rate_fluxes(self.dev.handle, n, ld, native.ptr(params),
+                                                native.ptr(conc), native.ptr(flux),
+                                                native.stream_handle()), 'vk_rate_fluxes')
+        return flux
+
+    def euler(self, dt, params, conc, mmol_to_counts, n_agents=None, flux=None, counts=None,
+              status=None, delta=None):
+        """Reference Euler step; returns (flux, counts, status).
+
+        ``delta=None`` updates ``conc`` in place; otherwise ``delta[n_dyn, ld]``
+        receives the reference update values and ``conc`` is left untouched."""
+        t = self.table
+        n = conc.shape[1] if n_agents is None else n_agents
+        ld = self._check_state(params, conc, n)
+        _need(mmol_to_counts, 'mmol_to_counts', None, ld, F64, self.device)
+        flux = self.empty_like_agents(t.n_reactions, ld) if flux is None else flux
+        counts = self.empty_like_agents(t.n_ext, ld, torch.int64) if counts is None else counts
+        status = self.empty_like_agents(None, ld, torch.int32) if status is None else status
+        _need(flux, 'flux', t.n_reactions, ld, F64, self.device)
+        _need(counts, 'counts', t.n_ext, ld, torch.int64, self.device)
+        _need(status, 'status', None, ld, torch.int32, self.device)
+        if delta is not None:
+            _need(delta, 'delta', t.n_dyn, ld, F64, self.device)
+        native.check(native._lib.vk_step_euler(
+            self.dev.handle, n, ld, float(dt), native.ptr(params), native.ptr(conc),
+            native.ptr(mmol_to_counts), native.ptr(delta), native.ptr(flux), native.ptr(counts),
+            native.ptr(status), native.stream_handle()), 'vk_step_euler')
+        return flux, counts, status
+
+    def dopri5(self, dt, params, conc, mmol_to_counts, n_agents=None, h_state=None, rtol=1e-8,
+               atol=1e-12, max_steps=100000, flux=None, counts=None, status=None, nsteps=None,
+               variant=0, delta=None):
+        """Adaptive DP5(4) over [0, dt] in place on ``conc``.
+
+        Returns (flux = mean flux over dt, counts, status, nsteps)."""
+        t = self.table
+        n = conc.shape[1] if n_agents is None else n_agents
+        ld = self._check_state(params, conc, n)
+        _need(mmol_to_counts, 'mmol_to_counts', None, ld, F64, self.device)
+        flux = self.empty_like_agents(t.n_reactions, ld) if flux is None else flux
+        counts = self.empty_like_agents(t.n_ext, ld, torch.int64) if counts is None else counts
+        status = self.empty_like_agents(None, ld, torch.int32) if status is None else status
+        nsteps = self.empty_like_agents(None, ld, torch.int32) if nsteps is None else nsteps
+        _need(flux, 'flux', t.n_reactions, ld, F64, self.device)
+        _need(counts, 'counts', t.n_ext, ld, torch.int64, self.device)
+        _need(status, 'status', None, ld, torch.int32, self.device)
+        _need(nsteps, 'nsteps', None, ld, torch.int32, self.device)
+        if h_state is not None:
+            _need(h_state, 'h_state', None, ld, F64, self.device)
+        if delta is not None:
+            _need(delta, 'delta', t.n_dyn, ld, F64, self.device)
+        opts = native.VkOdeOpts(float(rtol), float(atol), int(max_steps), int(variant))
+        native.check(native._lib.vk_step_dopri5(
+            self.dev.handle, n, ld, float(dt), ctypes.byref(opts), native.ptr(params),
+            native.ptr(conc), native.ptr(mmol_to_counts), native.ptr(delta), native.ptr(h_state),
+            native.ptr(flux),
+            native.ptr(counts), native.ptr(status), native.ptr(nsteps), native.stream_handle()),
+            'vk_step_dopri5')
+        return flux, counts, status, nsteps
+
+    # -- flop accounting (counted as the kernels execute) -----
+    def dopri5_flops_per_attempt(self) -> int:
+        """6 RHS evaluations + stage combinations + error norm per attempted step."""
+        ny = self.table.n_dyn + self.table.n_reactions
+        # stage inputs: 1+3+5+7+9 (a-rows with 1..5 terms: mul + fma chain + final fma),
+        # solution (5 terms): 11, error (6 terms + h*): 12, norm: max/abs/fma/div/fma ~ 6
+        per_component = 3 + 5 + 7 + 9 + 11 + 11 + 12 + 6
+        return 6 * self.table.flops_rhs() + per_component * ny

@@ -1,0 +1,197 @@
+"""Device-resident diffusion_field lattice (one row band per rank).
+
+Restates ``DiffusionField`` (vivarium/processes/diffusion_field.py:209-407)
+for a persistent SoA colony:
+
+* fields live in HBM as ``[n_fields, rows_local, ny]`` FP64 planes, where
+  ``rows_local = halo + owned + halo`` (axis 0 = x, as the reference's
+  ndarray); a single-GPU lattice has ``halo = 0``;
+* one step = the reference's ``diffusion_delta``: ``n_sub`` substeps of
+  0.01 s (100 / 501 / 1001 for dt = 1 / 5 / 10 s, the reference's float
+  accumulation quirk), uniform planes skipped, delta accumulated;
+* multi-rank: ``halo_exchange`` callbacks refresh ``halo`` rows every
+  ``halo`` substeps (k-deep halos) -- see
+  :mod:`lens_amd.distributed`.
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Optional, Sequence
+
+import torch
+
+from lens_amd import native
+
+N_A_LEGACY = 6.022140857e23   # constant the reference fixtures were produced with
+
+
+def n_substeps(timestep: float, dt_max: float = 0.01) -> int:
+    """Number of iterations of ``while t < timestep: t += dt`` (diffusion_field.py:388-392)."""
+    t, dt, n = 0.0, min(timestep, dt_max), 0
+    while t < timestep:
+        t += dt
+        n += 1
+    return n
+
+
+class Lattice:
+    def __init__(self, molecules: Sequence[str], n_bins, bounds, depth: float, diffusion: float,
+                 device=None, row_band=None, halo: int = 0, avogadro: float = N_A_LEGACY,
+                 initial=None):
+        self.molecules = list(molecules)
+        self.n_bins = [int(n_bins[0]), int(n_bins[1])]
+        self.bounds = [float(bounds[0]), float(bounds[1])]
+        self.depth = float(depth)
+        self.avogadro = float(avogadro)
+        nx, ny = self.n_bins
+        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        # DiffusionField.__init__ (diffusion_field.py:251-260)
+        dx = self.bounds[0] / nx
+        dy = self.bounds[1] / ny
+        self.diffusion = diffusion / (dx * dy)
+        self.diffusion_dt = 0.01
+        # get_bin_volume (lattice_utils.py:57-58); exchange divides by bin_volume*N_A
+        self.bin_volume = (self.depth * self.bounds[0] * self.bounds[1]) * 1e-15 / (nx * ny)
+        self.binvol_avogadro = self.bin_volume * self.avogadro
+        lo, hi = (0, nx) if row_band is None else (int(row_band[0]), int(row_band[1]))
+        if not (0 <= lo < hi <= nx):
+            raise ValueError('bad row band %r' % (row_band,))
+        self.row_lo_global, self.row_hi_global = lo, hi
+        self.halo = int(halo)
+        self.edge_top = lo == 0
+        self.edge_bot = hi == nx
+        h = self.halo
+        self.pad_top = 0 if self.edge_top else h
+        self.pad_bot = 0 if self.edge_bot else h
+        self.rows_local = self.pad_top + (hi - lo) + self.pad_bot
+        self.ny = ny
+        nf = len(self.molecules)
+        shape = (nf, self.rows_local, ny)
+        self.fields = torch.zeros(shape, dtype=torch.float64, device=self.device)
+        self.work0 = torch.empty(shape, dtype=torch.float64, device=self.device)
+        self.work1 = torch.empty(shape, dtype=torch.float64, device=self.device)
+        self.minmax = torch.empty(2 * max(nf, 1), dtype=torch.float64, device=self.device)
+        if initial is not None:
+            for f, m in enumerate(self.molecules):
+                if m in initial:
+                    self.set_field(m, initial[m])
+        else:
+            self.fields.fill_(1.0)   # DiffusionField.ones_field default (diffusion_field.py:381-382)
+
+    # local row index of the first owned row
+    @property
+    def row_lo(self) -> int:
+        return self.pad_top
+
+    @property
+    def row_hi(self) -> int:
+        return self.pad_top + (self.row_hi_global - self.row_lo_global)
+
+    @property
+    def field_stride(self) -> int:
+        return self.rows_local * self.ny
+
+    def set_field(self, molecule, values):
+        """Set the owned rows of a plane from a global [nx, ny] array/tensor."""
+        f = self.molecules.index(molecule)
+        v = torch.as_tensor(values, dtype=torch.float64)
+        if tuple(v.shape) != tuple(self.n_bins):
+            raise ValueError('field %s must be %s' % (molecule, self.n_bins))
+        band = v[self.row_lo_global:self.row_hi_global].to(self.device)
+        self.fields[f, self.row_lo:self.row_hi].copy_(band)
+
+    def owned(self, molecule=None):
+        sl = self.fields[:, self.row_lo:self.row_hi]
+        return sl if molecule is None else sl[self.molecules.index(molecule)]
+
+    # -- diffusion ------------------------------------------------------------
+    def uniform_minmax(self, allreduce: Optional[Callable] = None):
+        native.check(native._lib.vk_field_minmax(
+            native.ptr(self.fields), len(self.molecules), self.field_stride, self.ny, self.row_lo,
+            self.row_hi, native.ptr(self.minmax), native.stream_handle()), 'vk_field_minmax')
+        if allreduce is not None:
+            allreduce(self.minmax)
+        return self.minmax
+
+    def diffuse(self, timestep: float, halo_exchange: Optional[Callable] = None,
+                allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None):
+        """Advance every plane by ``timestep`` (diffusion_field.py:385-407).
+
+        ``events`` = (start, end) torch.cuda.Events recorded on the launch
+        stream around the substep kernels only (bench roofline timing)."""
+        n_sub = n_substeps(timestep, self.diffusion_dt)
+        coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
+        mm = self.uniform_minmax(allreduce) if skip_uniform else None
+        if events is not None:
+            events[0].record()
+        banded = bool(self.pad_top or self.pad_bot)
+        if banded and halo_exchange is None:
+            raise ValueError('a row band with halo rows needs a halo_exchange callback')
+        k = self.halo if banded else n_sub
+        lo_min = self.row_lo if self.edge_top else 0
+        hi_max = self.row_hi if self.edge_bot else self.rows_local
+        j = 0
+        while j < n_sub:
+            cnt = min(k, n_sub - j)
+            if banded:
+                # substep j reads src(j): field for j == 0, else work[(j-1) & 1]
+                src = self.fields if j == 0 else (self.work0 if ((j - 1) & 1) == 0 else self.work1)
+                halo_exchange(src, cnt)
+            native.check(native._lib.vk_diffuse(
+                native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1),
+                len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, lo_min,
+                hi_max, int(self.edge_top), int(self.edge_bot), j, cnt, n_sub, coeff_dt,
+                native.ptr(mm), native.stream_handle()), 'vk_diffuse')
+            j += cnt
+        if events is not None:
+            events[1].record()
+        return n_sub
+
+    # -- agent coupling ------------------------------------------------------
+    def bin_sites(self, loc, n_agents, bin_lin=None, ix=None):
+        """loc: [2, ld] float64 -> (bin_lin int32 [ld] local linear bin, ix int32 [ld])."""
+        ld = loc.shape[1]
+        bin_lin = torch.zeros(ld, dtype=torch.int32, device=self.device) if bin_lin is None else bin_lin
+        ix = torch.zeros(ld, dtype=torch.int32, device=self.device) if ix is None else ix
+        native.check(native._lib.vk_bin_sites(
+            native.ptr(loc), n_agents, ld, self.n_bins[0], self.n_bins[1], self.bounds[0],
+            self.bounds[1], self.row_lo_global - self.row_lo, native.ptr(bin_lin), native.ptr(ix),
+            native.stream_handle()), 'vk_bin_sites')
+        return bin_lin, ix
+
+    def gather(self, bin_lin, n_agents, map_field, map_row, dst):
+        """dst[map_row[i], a] = plane map_field[i] at bin_lin[a] (get_local_environments)."""
+        native.check(native._lib.vk_gather(
+            native.ptr(self.fields), self.field_stride, native.ptr(bin_lin), n_agents,
+            native.ptr(map_field), native.ptr(map_row), int(map_field.numel()), native.ptr(dst),
+            dst.shape[1], native.stream_handle()), 'vk_gather')
+
+    def exchange_sorted(self, occ, counts, map_count, map_field):
+        """Deterministic (agent-ordered) exchange; occ = (occ_bin, occ_ptr, occ_agent)."""
+        occ_bin, occ_ptr, occ_agent = occ
+        native.check(native._lib.vk_exchange_sorted(
+            native.ptr(self.fields), self.field_stride, native.ptr(occ_bin), native.ptr(occ_ptr),
+            native.ptr(occ_agent), int(occ_bin.numel()), native.ptr(counts), counts.shape[1],
+            native.ptr(map_count), native.ptr(map_field), int(map_count.numel()),
+            self.binvol_avogadro, native.stream_handle()), 'vk_exchange_sorted')
+
+    def exchange_atomic(self, bin_lin, n_agents, counts, map_count, map_field):
+        native.check(native._lib.vk_exchange_atomic(
+            native.ptr(self.fields), self.field_stride, native.ptr(bin_lin), n_agents,
+            native.ptr(counts), counts.shape[1], native.ptr(map_count), native.ptr(map_field),
+            int(map_count.numel()), self.binvol_avogadro, native.stream_handle()),
+            'vk_exchange_atomic')
+
+
+def occupancy(bin_lin: torch.Tensor, n_agents: int):
+    """Bin -> agents CSR in agent order (stable sort), for :meth:`Lattice.exchange_sorted`."""
+    b = bin_lin[:n_agents].to(torch.int64)
+    order = torch.sort(b, stable=True).indices
+    sb = b[order]
+    if n_agents == 0:
+        z = torch.zeros(0, dtype=torch.int32, device=bin_lin.device)
+        return z, torch.zeros(1, dtype=torch.int32, device=bin_lin.device), z
+    uniq, cnt = torch.unique_consecutive(sb, return_counts=True)
+    ptr = torch.zeros(uniq.numel() + 1, dtype=torch.int64, device=bin_lin.device)
+    ptr[1:] = torch.cumsum(cnt, 0)
+    return uniq.to(torch.int32), ptr.to(torch.int32), order.to(torch.int32)

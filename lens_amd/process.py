@@ -1,0 +1,206 @@
+"""Process-API drop-in: ``BatchedConvenienceKinetics``.
+
+Same ``name``, ``defaults``, ``ports_schema``, ``derivers`` and
+``next_update(timestep, states)`` contract as the reference
+``ConvenienceKinetics`` (vivarium/processes/convenience_kinetics.py:56-352),
+so it can replace it inside any Compartment / Experiment unchanged.  The
+update dict it returns is the reference's, key for key:
+
+* ``fluxes``: ``{reaction_id: flux}`` (updater ``set``),
+* per non-external port: ``{state: delta}`` accumulated in the reference's
+  order (``0 + sum_r coeff*flux*timestep``),
+* ``fields``: ``{mol: {'_value': int count, '_updater': {'updater':
+  'update_field_with_exchange', 'port_mapping': {...}}}}``.
+
+The arithmetic runs on the GPU (``vk_step_euler`` through the C ABI).  A
+single ``next_update`` call is a batch of one; :class:`lens_amd.invoke.
+BatchedInvoke` gathers every agent's call of a timestep into one launch.
+
+When the reference package is importable (its own Python 3.6-3.8
+environment) the class derives from ``vivarium.core.process.Process`` and
+registers in its ``process_registry``; otherwise from :class:`Process`
+below, a restatement of that base class (vivarium/core/process.py:201-306).
+"""
+
+from __future__ import annotations
+
+import copy
+import hashlib
+from typing import Any, Dict
+
+import numpy as np
+
+from lens_amd.rate_law_compiler import compile_rate_laws, RateLawTable
+
+DEFAULT_TIME_STEP = 1.0
+
+
+def deep_merge(dct, merge_dct):
+    """vivarium/library/dict_utils.py:51-65 (mutates and returns dct)."""
+    if dct is None:
+        dct = {}
+    if merge_dct is None:
+        merge_dct = {}
+    for k, v in merge_dct.items():
+        if k in dct and isinstance(dct[k], dict) and isinstance(v, dict):
+            deep_merge(dct[k], v)
+        else:
+            dct[k] = v
+    return dct
+
+
+class Process:
+    """Restatement of vivarium.core.process.Process (process.py:201-306)."""
+
+    defaults: Dict[str, Any] = {}
+    registry: Dict[str, type] = {}
+
+    def __init__(self, parameters=None):
+        assert hasattr(self, 'name')
+        if parameters is None:
+            parameters = {}
+        self.parameters = copy.deepcopy(self.defaults)
+        self.config = {}
+        self.schema_override = {}
+        if '_schema' in parameters:
+            self.schema_override = parameters.pop('_schema')
+        self.parallel = False
+        if '_parallel' in parameters:
+            self.parallel = parameters.pop('_parallel')
+        deep_merge(self.parameters, parameters)
+        Process.registry.setdefault(self.name, type(self))
+
+    def local_timestep(self):
+        return self.parameters.get('time_step', DEFAULT_TIME_STEP)
+
+    def ports(self):
+        return {port: list(states.keys()) for port, states in self.ports_schema().items()}
+
+    def default_state(self):
+        state = {}
+        for port, states in self.ports_schema().items():
+            for key, value in states.items():
+                if '_default' in value:
+                    state.setdefault(port, {})[key] = value['_default']
+        return state
+
+    def is_deriver(self):
+        return False
+
+    def derivers(self):
+        return {}
+
+    def ports_schema(self):
+        return {}
+
+    def next_update(self, timestep, states):
+        return {port: {} for port in self.ports()}
+
+
+try:  # the reference's own environment: be a real vivarium Process
+    from vivarium.core.process import Process as _VivariumProcess  # type: ignore
+    ProcessBase = _VivariumProcess
+except Exception:  # pragma: no cover - the reference is not installed here
+    ProcessBase = Process
+
+
+def _magnitude(x):
+    """units.remove_units for a scalar (vivarium/library/units.py:37-65)."""
+    return getattr(x, 'magnitude', x)
+
+
+def table_signature(table: RateLawTable) -> str:
+    """Processes whose compiled tables are structurally identical share one batch."""
+    h = hashlib.sha1()
+    h.update(repr((table.species, table.n_dyn, table.reaction_ids, table.external_ids,
+                   table.param_names and [p[0] for p in table.param_names])).encode())
+    for name, arr in table.arrays().items():
+        h.update(name.encode())
+        h.update(np.ascontiguousarray(arr).tobytes())
+    return h.hexdigest()
+
+
+class BatchedConvenienceKinetics(ProcessBase):
+    """GPU-batched drop-in for ``ConvenienceKinetics``."""
+
+    name = 'convenience_kinetics'
+    defaults = {
+        'reactions': {},
+        'initial_state': {'internal': {}, 'external': {}},
+        'kinetic_parameters': {},
+        'port_ids': ['internal', 'external'],
+        'added_port_ids': ['fluxes', 'fields', 'global'],
+        'global_deriver_key': 'global_deriver',
+    }
+
+    def __init__(self, parameters=None):
+        super().__init__(parameters)
+        self.reactions = self.parameters['reactions']
+        self.initial_state = self.parameters['initial_state']
+        self.kinetic_parameters = self.parameters['kinetic_parameters']
+        self.port_ids = self.parameters['port_ids'] + self.parameters['added_port_ids']
+        self.table = compile_rate_laws(self.reactions, self.kinetic_parameters, self.port_ids)
+        self.signature = table_signature(self.table)
+        self.param_values = self.table.param_defaults.copy()
+
+    # -- schema: convenience_kinetics.py:240-301 --------------------------------
+    def ports_schema(self):
+        schema = {port_id: {} for port_id in self.port_ids}
+        for port, states in self.initial_state.items():
+            for state_id in states:
+                schema.setdefault(port, {})[state_id] = {
+                    '_default': self.initial_state[port][state_id], '_emit': True}
+        if 'external' in schema:
+            schema['fields'] = {state_id: {'_default': np.ones((1, 1))}
+                                for state_id in schema['external'].keys()}
+        for rid in self.table.reaction_ids:
+            schema['fluxes'][rid] = {'_default': 0.0, '_emit': False, '_updater': 'set'}
+        schema['global'] = {
+            'mmol_to_counts': {'_default': 0.0, '_emit': False},
+            'location': {'_default': [0.5, 0.5]},
+        }
+        schema['dimensions'] = {
+            'bounds': {'_default': [1, 1]},
+            'n_bins': {'_default': [1, 1]},
+            'depth': {'_default': 1},
+        }
+        return schema
+
+    def derivers(self):
+        return {
+            self.parameters['global_deriver_key']: {
+                'deriver': 'globals_deriver',
+                'port_mapping': {'global': 'global'},
+                'config': {'width': 1.0}}}
+
+    # -- packing helpers shared with BatchedInvoke ----------------------------
+    def pack_state(self, states, conc_col: np.ndarray):
+        """Write one agent's species values into a [n_species] column."""
+        for s, (port, name) in enumerate(self.table.species):
+            v = states.get(port, {})
+            v = v.get(name, 0.0) if isinstance(v, dict) else 0.0
+            conc_col[s] = float(_magnitude(v))
+        return float(_magnitude(states['global']['mmol_to_counts']))
+
+    def unpack_update(self, fluxes_col, delta_col, counts_col):
+        """Device outputs of one agent -> the reference's update dict
+        (convenience_kinetics.py:316-349)."""
+        t = self.table
+        update = {port: {} for port in self.port_ids}
+        update['fluxes'] = {rid: np.float64(fluxes_col[r]) for r, rid in enumerate(t.reaction_ids)}
+        for s in range(t.n_dyn):
+            port, name = t.species[s]
+            update.setdefault(port, {})[name] = float(delta_col[s])
+        for e, mol in enumerate(t.external_ids):
+            update['fields'][mol] = {
+                '_value': int(counts_col[e]),
+                '_updater': {
+                    'updater': 'update_field_with_exchange',
+                    'port_mapping': {'global': 'global', 'dimensions': 'dimensions'},
+                },
+            }
+        return update
+
+    def next_update(self, timestep, states):
+        from lens_amd.invoke import run_batch
+        return run_batch([(self, timestep, states)])[0]

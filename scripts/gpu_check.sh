@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU session: tests, smoke, short bench, kernel-trace profile.  Every GPU
+# step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS=${STEPS:-5}
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -5 gpurun_out/pytest_gpu.log
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 3; }
+tail -2 gpurun_out/smoke.log
+timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 4; }
+tail -1 gpurun_out/bench.log

@@ -1,0 +1,355 @@
+"""HIP path vs the oracle, through the C ABI (needs an MI355X)."""
+
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+from netcodec import decode_network, decode_conc  # noqa: E402
+from table_eval import table_euler  # noqa: E402
+from lens_amd import configs  # noqa: E402
+from lens_amd.rate_law_compiler import compile_rate_laws  # noqa: E402
+from oracle import cpu  # noqa: E402
+from oracle import lattice as olat  # noqa: E402
+from oracle.kinetics import OracleODE, OracleAgent, mmol_to_counts, replay_single_agent  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda', 0)
+
+
+def _soa(t, concs):
+    return np.ascontiguousarray(np.array([[float(c.get(k, 0.0)) for c in concs] for k in t.species]))
+
+
+def _engine(t, dev):
+    from lens_amd.kinetics import KineticsEngine
+    return KineticsEngine(t, dev)
+
+
+def test_library_is_the_hip_build(dev):
+    from lens_amd import native
+    lib = native.load()
+    assert lib.vk_abi_version() == 1
+    assert os.path.samefile(native.LIB_PATH, os.path.join(os.path.dirname(native.__file__), 'lib',
+                                                          'libvk_kinetics.so'))
+
+
+def test_rate_fluxes_bitwise_vs_reference(dev, golden_fluxes):
+    for case in golden_fluxes['cases']:
+        rx, kp = decode_network(case['network'])
+        t = compile_rate_laws(rx, kp)
+        concs = [decode_conc(c) for c in case['concs']]
+        n = len(concs)
+        eng = _engine(t, dev)
+        ld = n + 3  # exercise ld > n
+        conc = np.zeros((t.n_species, ld))
+        conc[:, :n] = _soa(t, concs)
+        params = np.repeat(t.param_defaults[:, None], ld, axis=1)
+        flux = eng.fluxes(torch.from_numpy(params).to(dev), torch.from_numpy(conc).to(dev), n_agents=n)
+        got = flux.cpu().numpy()[:, :n]
+        expect = np.array([[f[r] for f in case['fluxes']] for r in t.reaction_ids])
+        assert np.array_equal(got, expect), case['name']
+
+
+def test_euler_step_bitwise(dev, golden_fluxes):
+    rng = np.random.default_rng(11)
+    for case in golden_fluxes['cases']:
+        rx, kp = decode_network(case['network'])
+        t = compile_rate_laws(rx, kp)
+        concs = [decode_conc(c) for c in case['concs']]
+        n = len(concs)
+        conc = _soa(t, concs)
+        params = np.ascontiguousarray(np.repeat(t.param_defaults[:, None], n, axis=1))
+        m2c = rng.uniform(1e5, 1e6, n)
+        dt = 1.0
+        eng = _engine(t, dev)
+        c_dev = torch.from_numpy(conc.copy()).to(dev)
+        delta = torch.zeros((t.n_dyn, n), dtype=torch.float64, device=dev)
+        flux, counts, status = eng.euler(dt, torch.from_numpy(params).to(dev), c_dev,
+                                         torch.from_numpy(m2c).to(dev), delta=delta)
+        # delta mode leaves conc untouched
+        assert np.array_equal(c_dev.cpu().numpy(), conc)
+        flux2, counts2, _ = eng.euler(dt, torch.from_numpy(params).to(dev), c_dev,
+                                      torch.from_numpy(m2c).to(dev))
+        new = c_dev.cpu().numpy()
+        for a in range(n):
+            agent = OracleAgent(rx, kp)
+            states = {}
+            for (port, name), v in concs[a].items():
+                states.setdefault(port, {})[name] = v
+            fl, deltas, cnt = agent.next_update(dt, states, m2c[a])
+            for s in range(t.n_dyn):
+                port, name = t.species[s]
+                assert delta.cpu().numpy()[s, a] == deltas[port][name]
+                assert new[s, a] == conc[s, a] + deltas[port][name]
+            assert counts.cpu().numpy()[:, a].tolist() == [cnt[e] for e in t.external_ids]
+            assert flux.cpu().numpy()[:, a].tolist() == [fl[r] for r in t.reaction_ids]
+        assert not status.cpu().numpy().any()
+
+
+def test_c1_colony_reproduces_reference_csv(dev):
+    """BASELINE config 1 on the GPU: 2520 Euler steps == convenience_kinetics.csv."""
+    import csv
+    from lens_amd.colony import Colony
+    cfg = configs.glc_lct_config()
+    col = Colony(cfg, 1, device=dev, integrator='euler', environment='nonspatial')
+    rows = {int(float(r['time'])): r for r in csv.DictReader(open(os.path.join(GOLDEN, 'convenience_kinetics_subset.csv')))}
+    for step in range(2521):
+        if step in rows:
+            snap = col.snapshot()
+            row = rows[step]
+            for port in ('internal', 'external'):
+                for name, v in snap[port].items():
+                    ref = float(row[port + '_' + name])
+                    if port == 'internal':
+                        assert abs(v[0] - ref) <= 1e-14 * abs(ref), (step, name)
+                    else:
+                        assert abs(v[0] - ref) <= 1e-15, (step, name)
+        if step < 2520:
+            col.step(1.0)
+
+
+def _params_dict(t, cfg, pvec):
+    kp = {}
+    for (kind, rid, enz, *mol), v in zip(t.param_names, pvec):
+        kp.setdefault(rid, {}).setdefault(enz, {})
+        kp[rid][enz]['kcat_f' if kind == 'kcat' else mol[0]] = float(v)
+    for rid in cfg['kinetic_parameters']:
+        for enz, p in cfg['kinetic_parameters'][rid].items():
+            for k, v in p.items():
+                if v is None:
+                    kp[rid][enz][k] = None
+    return kp
+
+
+@pytest.mark.parametrize('name', ['glc_lct', 'glc_ac', 'glc_lct_transport'])
+def test_dopri5_matches_odeint(dev, name):
+    """North-star bar: end states within 1e-6 relative of scipy odeint (LSODA)."""
+    cfg = {'glc_lct': configs.glc_lct_config, 'glc_ac': configs.glc_ac_config,
+           'glc_lct_transport': configs.glc_lct_transport_config}[name]()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    n = 300
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=5)
+    m2c = np.full(n, mmol_to_counts())
+    eng = _engine(t, dev)
+    c_dev = torch.from_numpy(conc.copy()).to(dev)
+    h = torch.zeros(n, dtype=torch.float64, device=dev)
+    flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
+                                              torch.from_numpy(m2c).to(dev), h_state=h)
+    assert not status.cpu().numpy().any()
+    got = c_dev.cpu().numpy()
+    fl = flux.cpu().numpy()
+    for a in range(0, n, 23):
+        ode = OracleODE(cfg['reactions'], _params_dict(t, cfg, params[:, a]))
+        new, mean_flux, cnt = ode.step({k: conc[s, a] for s, k in enumerate(t.species)}, 1.0, m2c[a])
+        for s in range(t.n_dyn):
+            ref = new[t.species[s]]
+            assert abs(got[s, a] - ref) <= 1e-6 * abs(ref) + 1e-12, (name, a, t.species[s], got[s, a], ref)
+        for r, rid in enumerate(t.reaction_ids):
+            assert abs(fl[r, a] - mean_flux[rid]) <= 1e-6 * abs(mean_flux[rid]) + 1e-12
+
+
+def test_dopri5_matches_c_oracle_all_agents(dev):
+    cfg = configs.glc_lct_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    n = 5000
+    params, conc = configs.heterogeneous_colony(t, cfg, n)
+    m2c = np.full(n, mmol_to_counts())
+    eng = _engine(t, dev)
+    c_dev = torch.from_numpy(conc.copy()).to(dev)
+    flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
+                                              torch.from_numpy(m2c).to(dev))
+    c_ref = conc.copy()
+    f_ref, k_ref, s_ref, n_ref = cpu.step_dopri5(cpu.Desc(t), 1.0, params, c_ref, m2c)
+    got = c_dev.cpu().numpy()
+    rel = np.abs(got[:t.n_dyn] - c_ref[:t.n_dyn]) / (np.abs(c_ref[:t.n_dyn]) + 1e-300)
+    assert rel.max() < 1e-10
+    # same algorithm, same step sequence
+    assert np.mean(nsteps.cpu().numpy() == n_ref) > 0.99
+
+
+def test_dopri5_status_and_limits(dev):
+    from lens_amd.native import NativeError
+    cfg = configs.glc_lct_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    params, conc = configs.heterogeneous_colony(t, cfg, 64)
+    eng = _engine(t, dev)
+    c_dev = torch.from_numpy(conc).to(dev)
+    _, _, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
+                                      torch.full((64,), 7e5, dtype=torch.float64, device=dev),
+                                      max_steps=1, rtol=1e-12, atol=1e-16)
+    assert (status.cpu().numpy() & 1).any()
+    # zero agents is a no-op
+    eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
+               torch.full((64,), 7e5, dtype=torch.float64, device=dev), n_agents=0)
+    # a 50-species network exceeds the agent-per-thread variant
+    big = configs.synthetic_network(n_species=60, n_reactions=40)
+    tb = compile_rate_laws(big['reactions'], big['kinetic_parameters'])
+    eb = _engine(tb, dev)
+    pb = torch.from_numpy(np.repeat(tb.param_defaults[:, None], 8, axis=1)).to(dev)
+    cb = torch.ones((tb.n_species, 8), dtype=torch.float64, device=dev)
+    if tb.n_dyn + tb.n_reactions > 32:
+        with pytest.raises(NativeError):
+            eb.dopri5(1.0, pb, cb, torch.ones(8, dtype=torch.float64, device=dev))
+    with pytest.raises(ValueError):
+        eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev[:, :10].contiguous(),
+                   torch.ones(64, dtype=torch.float64, device=dev))
+
+
+def test_stencil_bitwise_vs_scipy_convolve(dev):
+    from lens_amd.lattice import Lattice
+    z = np.load(os.path.join(GOLDEN, 'stencil.npz'))
+    for shape in ('17x23', '64x64', '128x96'):
+        f0 = z['f0_' + shape]
+        nx, ny = f0.shape
+        for dt in (1.0, 5.0, 10.0):
+            lat = Lattice(['a', 'b'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                          initial={'a': f0, 'b': np.full((nx, ny), 2.5)})
+            n_sub = lat.diffuse(dt)
+            assert n_sub == int(z['n_%s_dt%g' % (shape, dt)])
+            assert np.array_equal(lat.owned('a').cpu().numpy(), z['f_%s_dt%g' % (shape, dt)])
+            assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))  # uniform skip
+
+
+def test_single_substep_diffusion(dev):
+    from lens_amd.lattice import Lattice
+    rng = np.random.default_rng(2)
+    f0 = rng.random((20, 30))
+    lat = Lattice(['a'], (20, 30), (20.0, 30.0), 10.0, 5.0, device=dev, initial={'a': f0})
+    lat.diffuse(0.005)   # one substep (dt < 0.01)
+    ref = olat.diffuse(f0, 0.005, 5.0, (20, 30), (20.0, 30.0))
+    assert np.array_equal(lat.owned('a').cpu().numpy(), ref)
+
+
+def test_banded_diffusion_equals_whole(dev):
+    """Row bands with k-deep halos (the multi-GPU decomposition) on one device."""
+    from lens_amd.lattice import Lattice
+    rng = np.random.default_rng(3)
+    nx, ny = 97, 40
+    f0 = rng.random((nx, ny)) * 5
+    whole = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+    whole.diffuse(1.0)
+    for world, halo in ((2, 8), (3, 5), (4, 1), (3, 16)):
+        from lens_amd.distributed import row_bands
+        bands = row_bands(nx, world)
+        lats = [Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                        row_band=b, halo=halo, initial={'a': f0}) for b in bands]
+
+        def make_ex(r):
+            def ex(src, cnt):
+                lat = lats[r]
+                names = {id(lat.fields): 'fields', id(lat.work0): 'work0', id(lat.work1): 'work1'}
+                which = names[id(src)]
+                if not lat.edge_top:
+                    nb = lats[r - 1]
+                    s = getattr(nb, which)
+                    src[:, lat.row_lo - halo:lat.row_lo].copy_(s[:, nb.row_hi - halo:nb.row_hi])
+                if not lat.edge_bot:
+                    nb = lats[r + 1]
+                    s = getattr(nb, which)
+                    src[:, lat.row_hi:lat.row_hi + halo].copy_(s[:, nb.row_lo:nb.row_lo + halo])
+            return ex
+
+        # lock-step: every band runs block j before any runs block j+1
+        from lens_amd import native
+        n_sub = 100
+        coeff_dt = lats[0].diffusion * 0.01
+        j = 0
+        while j < n_sub:
+            cnt = min(halo, n_sub - j)
+            for r, lat in enumerate(lats):
+                src = lat.fields if j == 0 else (lat.work0 if ((j - 1) & 1) == 0 else lat.work1)
+                make_ex(r)(src, cnt)
+            for lat in lats:
+                lo_min = lat.row_lo if lat.edge_top else 0
+                hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
+                native.check(native._lib.vk_diffuse(
+                    native.ptr(lat.fields), native.ptr(lat.work0), native.ptr(lat.work1), 1,
+                    lat.field_stride, ny, lat.row_lo, lat.row_hi, lo_min, hi_max, int(lat.edge_top),
+                    int(lat.edge_bot), j, cnt, n_sub, coeff_dt, 0, native.stream_handle()), 'diffuse')
+            j += cnt
+        got = torch.cat([lat.owned('a') for lat in lats], 0).cpu().numpy()
+        assert np.array_equal(got, whole.owned('a').cpu().numpy()), (world, halo)
+
+
+def test_lattice_colony_step_vs_oracle(dev):
+    """Gather (pre-step) -> diffusion -> agent-ordered exchange, bit-exact, with a
+    bin shared by several agents."""
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    cfg = configs.glc_ac_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    nx, ny, n = 24, 20, 200
+    bounds = (24.0, 20.0)
+    glc = configs.gaussian_bump_field((nx, ny))
+    ac = np.zeros((nx, ny))
+    rng = np.random.default_rng(9)
+    loc = np.stack([rng.uniform(0, bounds[0], n), rng.uniform(0, bounds[1], n)])
+    loc[:, 5] = loc[:, 3]  # agents 3 and 5 share a bin
+    for exchange in ('sorted', 'atomic'):
+        lat = Lattice(['glc__D_e', 'ac_e'], (nx, ny), bounds, 10.0, 5.0, device=dev,
+                      initial={'glc__D_e': glc, 'ac_e': ac})
+        col = Colony(cfg, n, device=dev, integrator='euler', environment=lat, table=t, exchange=exchange)
+        params, conc = configs.heterogeneous_colony(t, cfg, n, seed=4)
+        col.set_agents(params=params, conc=conc, location=loc)
+        col.gather_external()
+        conc0 = col.conc.cpu().numpy().copy()
+        col.step(1.0)
+        # oracle: Euler per agent (table order) + lattice_step in agent order
+        m2c = col.m2c.cpu().numpy()
+        counts = {m: [] for m in t.external_ids}
+        for a in range(n):
+            _, _, cnt = table_euler(t, conc0[:, a], params[:, a], 1.0, m2c[a])
+            for e, m in enumerate(t.external_ids):
+                counts[m].append(int(cnt[e]))
+        new, local = olat.lattice_step({'glc__D_e': glc.copy(), 'ac_e': ac.copy()},
+                                       [tuple(loc[:, a]) for a in range(n)], counts, (nx, ny), bounds,
+                                       10.0, 1.0, 5.0)
+        got_g = lat.owned('glc__D_e').cpu().numpy()
+        if exchange == 'sorted':
+            assert np.array_equal(got_g, new['glc__D_e'])
+            assert np.array_equal(lat.owned('ac_e').cpu().numpy(), new['ac_e'])
+        else:
+            np.testing.assert_allclose(got_g, new['glc__D_e'], rtol=1e-14, atol=0)
+        ext = col.species('external', 'glc__D_e').cpu().numpy()
+        assert np.array_equal(ext, local['glc__D_e'])
+
+
+def test_process_drop_in_update_dict(dev):
+    from lens_amd.process import BatchedConvenienceKinetics
+    from lens_amd.invoke import BatchedInvoke
+    cfg = configs.glc_lct_config()
+    proc = BatchedConvenienceKinetics(cfg)
+    states = {'internal': dict(cfg['initial_state']['internal']),
+              'external': {'glc__D_e': 3.0, 'lcts_e': 2.0},
+              'fluxes': {}, 'fields': {}, 'global': {'mmol_to_counts': 733058.77, 'location': [0.5, 0.5]},
+              'dimensions': {}}
+    update = proc.next_update(1.0, states)
+    agent = OracleAgent(cfg['reactions'], cfg['kinetic_parameters'])
+    fl, deltas, counts = agent.next_update(1.0, states, 733058.77)
+    assert update['fluxes'] == fl
+    assert update['internal'] == {k: v for k, v in deltas['internal'].items()}
+    assert {m: v['_value'] for m, v in update['fields'].items()} == counts
+    assert update['fields']['glc__D_e']['_updater']['updater'] == 'update_field_with_exchange'
+    # batched: many processes, one launch per (network, interval)
+    inv = BatchedInvoke()
+    procs = [BatchedConvenienceKinetics(cfg) for _ in range(50)]
+    futs = []
+    for i, p in enumerate(procs):
+        st = {**states, 'external': {'glc__D_e': 0.1 * (i + 1), 'lcts_e': 1.0}}
+        futs.append((inv(p, 1.0, st), st))
+    for f, st in futs:
+        got = f.get()
+        fl, deltas, counts = agent.next_update(1.0, st, 733058.77)
+        assert got['fluxes'] == fl and got['internal'] == deltas['internal']
+        assert {m: v['_value'] for m, v in got['fields'].items()} == counts
