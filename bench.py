@@ -150,13 +150,17 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
-        col.step(1.0, halo_exchange=halo_ex, allreduce=allred)
-    col.check_status()
     ev = lambda: torch.cuda.Event(enable_timing=True)
     timing = [{'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())}
-              for _ in range(args.steps)]
+              for _ in range(max(args.steps, args.warmup))]
     nsteps_acc = torch.zeros((), dtype=torch.int64, device=dev)
+    # warmup runs exactly the timed loop body (first-use costs land here)
+    for k in range(args.warmup):
+        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing[k])
+        nsteps_acc += col.nsteps[:col.n].sum()
+    barrier()
+    col.check_status()
+    nsteps_acc.zero_()
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):

@@ -215,6 +215,16 @@ def synthetic_network(n_species=50, n_reactions=40, n_enzymes=10, seed=SEED,
         p = {m: float(10 ** rng.uniform(-3, 1)) for m in subs}
         p['kcat_f'] = float(10 ** rng.uniform(-1, 4))
         kinetics[rid] = {enz: p}
+    # an enzyme's partition holds the substrates of every reaction it catalyses
+    # (kinetic_rate_laws.py:84-95), so each of its rate laws needs their Kms
+    for rid, spec in reactions.items():
+        enz = spec['catalyzed by'][0]
+        p = kinetics[rid][enz]
+        for other in reactions.values():
+            if enz in other['catalyzed by']:
+                for m, c in other['stoichiometry'].items():
+                    if c < 0 and m not in p:
+                        p[m] = float(10 ** rng.uniform(-3, 1))
     initial = {'internal': {k[1]: float(rng.uniform(0.1, 2.0)) for k in internal},
                'external': {k[1]: float(rng.uniform(1.0, 10.0)) for k in external}}
     for e in enzymes:
