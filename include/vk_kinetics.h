@@ -165,6 +165,17 @@ int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
                const double *minmax, vk_stream_t stream);
 
+/* Substeps fused per HBM pass by vk_diffuse (temporal blocking; odd, 1..15;
+ * 1 = one launch per substep).  Returns the previous value; k outside 1..15
+ * only queries.  Results are bit-identical for every depth.               */
+int vk_set_stencil_depth(int32_t k);
+
+/* Fused-pass kernel variant: 0 = workgroup tile with an LDS neighbour
+ * exchange, 1 = wave tile with DPP lane shifts (default); rows = output rows
+ * per tile (8..4096; other values keep the current).  Returns the previous
+ * variant.  Tuning only: results are bit-identical for every setting.     */
+int vk_set_stencil_kernel(int32_t variant, int32_t rows);
+
 /* dst[map_row[i]*ld + a] = fields[map_field[i]*field_stride + bin_lin[a]]. */
 int vk_gather(const double *fields, int64_t field_stride, const int32_t *bin_lin,
               int64_t n_agents, const int32_t *map_field, const int32_t *map_row,

@@ -65,6 +65,356 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
     }
 }
 
+// ---------------------------------------------------------------------------
+// Temporally blocked stencil: K substeps per pass over HBM.
+//
+// A workgroup owns a tile of TB_BX columns (TB_BX-2K output columns + K halo
+// columns per side) and a chunk of output rows; it streams its input rows
+// top to bottom once.  Substep s (0-based) is a pipeline stage holding a
+// three-row window (up, centre, newest) per column in VGPRs; at iteration i
+// stage s produces row i-2s-1, and its output becomes stage s+1's newest
+// row in iteration i+1, so all K stages of an iteration are independent and
+// share ONE LDS exchange of centre values (left/right neighbours) and ONE
+// barrier (LDS double-buffered by iteration parity).  HBM traffic per pass:
+// one read of (chunk+2K) rows and one write of chunk rows, instead of K reads
+// and K writes.  The arithmetic per cell and substep is the reference's
+// ((up + left) + (-4*c)) + right) + down, c + coef*lap -- fma(-4, c, s) is
+// bit-identical to s + (-4*c) because -4*c is exact.
+// ---------------------------------------------------------------------------
+
+constexpr int TB_BX = 256;
+
+// One pipeline iteration with static register roles U (loop unrolled by 3, so
+// the three-row windows rotate by renaming instead of v_mov).  For stage q:
+// up = X[U], centre = X[U+1], newest = X[U+2] (mod 3); stage q-1's output is
+// stage q's newest next iteration and lands in X[U] once stage q consumed it.
+template <int K, bool EDGE, int U>
+__device__ __forceinline__ void tb_iter(double (&xch)[2][K][TB_BX], double (&X0)[K], double (&X1)[K],
+                                        double (&X2)[K], double (&pf)[3], const double *__restrict__ s,
+                                        double *__restrict__ d, const double *__restrict__ g, int ny, int i,
+                                        int c0, int c1, int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                        int c, int cc, bool writer, int tl, int tr, bool left_edge,
+                                        bool right_edge, double coef) {
+    double(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
+    double(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
+    double(&NW)[K] = U == 0 ? X2 : (U == 1 ? X0 : X1);
+    const int tid = threadIdx.x;
+    NW[0] = pf[U];                                                    // row i, loaded 3 iterations ago
+    pf[U] = s[(int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny + cc];  // prefetch row i+3
+    const int r_out = i - 2 * K + 1;
+    const bool do_write = writer && r_out >= c0 && r_out < c1;
+    double base = 0.0;
+    if (g && do_write) base = g[(int64_t)r_out * ny + c];
+    const int p = i & 1;
+#pragma unroll
+    for (int q = 0; q < K; ++q) xch[p][q][tid] = CN[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = K - 1; q >= 0; --q) {
+        const int r = i - 2 * q - 1;
+        const double cen = CN[q];
+        const double up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double dn = (EDGE && r == bot_reflect) ? cen : NW[q];
+        const double lv = xch[p][q][tl], rv = xch[p][q][tr];
+        const double lf = left_edge ? cen : lv;
+        const double rt = right_edge ? cen : rv;
+        const double lap = ((fma(-4.0, cen, up + lf)) + rt) + dn;
+        const double v = cen + coef * lap;
+        if (q + 1 < K) {
+            UP[q + 1] = v;
+        } else if (do_write) {
+            d[(int64_t)r_out * ny + c] = g ? base + (v - base) : v;
+        }
+    }
+}
+
+// EDGE = the tile touches a reflecting boundary (global edge rows/columns);
+// interior tiles (the vast majority) carry no boundary selects at all.
+template <int K, bool EDGE>
+__device__ __forceinline__ void diffuse_tb_body(double (&xch)[2][K][TB_BX], const double *__restrict__ s,
+                                                double *__restrict__ d, const double *__restrict__ g, int ny,
+                                                int c0, int c1, int in_lo, int in_hi, int top_reflect,
+                                                int bot_reflect, int x0, double coef) {
+    const int tid = threadIdx.x;
+    const int c = x0 - K + tid;
+    const int cc = min(max(c, 0), ny - 1);
+    const bool left_edge = EDGE && (c == 0), right_edge = EDGE && (c == ny - 1);
+    const bool writer = tid >= K && tid < TB_BX - K && c < ny;
+    const int tl = max(tid - 1, 0), tr = min(tid + 1, TB_BX - 1);
+
+    double X0[K], X1[K], X2[K], pf[3];
+#pragma unroll
+    for (int q = 0; q < K; ++q) X0[q] = X1[q] = X2[q] = 0.0;
+    const int i0 = c0 - K, i1 = c1 + 2 * K - 1;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) pf[u] = s[(int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny + cc];
+#define TB_ARGS xch, X0, X1, X2, pf, s, d, g, ny
+#define TB_REST c0, c1, in_lo, in_hi, top_reflect, bot_reflect, c, cc, writer, tl, tr, left_edge, right_edge, coef
+    int i = i0;
+    for (; i + 3 <= i1; i += 3) {
+        tb_iter<K, EDGE, 0>(TB_ARGS, i, TB_REST);
+        tb_iter<K, EDGE, 1>(TB_ARGS, i + 1, TB_REST);
+        tb_iter<K, EDGE, 2>(TB_ARGS, i + 2, TB_REST);
+    }
+    if (i < i1) tb_iter<K, EDGE, 0>(TB_ARGS, i, TB_REST);
+    if (i + 1 < i1) tb_iter<K, EDGE, 1>(TB_ARGS, i + 1, TB_REST);
+#undef TB_ARGS
+#undef TB_REST
+}
+
+template <int K>
+__global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__ src, double *__restrict__ dst,
+                                                      const double *__restrict__ f0, int64_t field_stride, int ny,
+                                                      int out_lo, int out_hi, int in_lo, int in_hi,
+                                                      int top_reflect, int bot_reflect, int rows_per_chunk,
+                                                      double coef, const double *__restrict__ minmax) {
+    const int f = blockIdx.z;
+    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;  // uniform plane: zero delta
+    const int c0 = out_lo + blockIdx.y * rows_per_chunk;
+    if (c0 >= out_hi) return;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = blockIdx.x * (TB_BX - 2 * K);
+    __shared__ double xch[2][K][TB_BX];
+    const double *s = src + (int64_t)f * field_stride;
+    double *d = dst + (int64_t)f * field_stride;
+    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    // rows this block touches: [c0-K-1, c1+2K); columns [x0-K-1, x0-K+TB_BX]
+    const bool edge = (x0 - K - 1 <= 0) || (x0 - K + TB_BX >= ny - 1) ||
+                      (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
+                      (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
+    if (edge)
+        diffuse_tb_body<K, true>(xch, s, d, g, ny, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, x0, coef);
+    else
+        diffuse_tb_body<K, false>(xch, s, d, g, ny, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, x0, coef);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-tile variant: one wavefront = one independent tile of 128 columns (two
+// adjacent columns per lane), so there is no LDS and no barrier at all.  The
+// left/right neighbours come from the lane itself (A<->B) and from the
+// adjacent lanes through DPP wave shifts (v_mov_b32_dpp wave_shr:1 /
+// wave_shl:1); the tile's outer KH columns per side are the halo that the K
+// fused substeps eat into.  Loads/stores are 16 B per lane.
+// ---------------------------------------------------------------------------
+
+constexpr int WT_COLS = 128;
+
+__device__ __forceinline__ double dpp_from_lane_below(double v) {  // lane l <- lane l-1
+    int2 x = __builtin_bit_cast(int2, v);
+    int2 y;
+    y.x = __builtin_amdgcn_update_dpp(0, x.x, 0x138, 0xf, 0xf, false);
+    y.y = __builtin_amdgcn_update_dpp(0, x.y, 0x138, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, y);
+}
+
+__device__ __forceinline__ double dpp_from_lane_above(double v) {  // lane l <- lane l+1
+    int2 x = __builtin_bit_cast(int2, v);
+    int2 y;
+    y.x = __builtin_amdgcn_update_dpp(0, x.x, 0x130, 0xf, 0xf, false);
+    y.y = __builtin_amdgcn_update_dpp(0, x.y, 0x130, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, y);
+}
+
+struct WtLane {
+    int cA;              // this lane's first column (cB = cA + 1)
+    int ny;
+    bool wA, wB;         // writes its column A / B
+    bool lA, rA, lB, rB; // reflect flags (EDGE tiles only)
+};
+
+template <bool EDGE>
+__device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t row_off, const WtLane &L) {
+    if (!EDGE) return *reinterpret_cast<const double2 *>(p + row_off + L.cA);
+    const int a = min(max(L.cA, 0), L.ny - 1), b = min(max(L.cA + 1, 0), L.ny - 1);
+    return make_double2(p[row_off + a], p[row_off + b]);
+}
+
+template <int K, bool EDGE, int U>
+__device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], double2 (&X2)[K], double2 (&pf)[3],
+                                        const double *__restrict__ s, double *__restrict__ d,
+                                        const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    double2(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
+    double2(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
+    double2(&NW)[K] = U == 0 ? X2 : (U == 1 ? X0 : X1);
+    const int64_t ny = L.ny;
+    NW[0] = pf[U];                                                                   // row i
+    pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny, L);  // prefetch row i+3
+    const int r_out = i - 2 * K + 1;
+    const bool row_ok = r_out >= c0 && r_out < c1;
+    double2 base = make_double2(0.0, 0.0);
+    if (g && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
+#pragma unroll
+    for (int q = K - 1; q >= 0; --q) {
+        const int r = i - 2 * q - 1;
+        const double2 cen = CN[q];
+        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double2 dn = (EDGE && r == bot_reflect) ? cen : NW[q];
+        double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
+        double rightA = cen.y, leftB = cen.x;
+        if (EDGE) {
+            leftA = L.lA ? cen.x : leftA;
+            rightA = L.rA ? cen.x : rightA;
+            leftB = L.lB ? cen.y : leftB;
+            rightB = L.rB ? cen.y : rightB;
+        }
+        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
+        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
+        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
+        if (q + 1 < K) {
+            UP[q + 1] = v;
+        } else if (row_ok) {
+            if (g) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            double *o = d + (int64_t)r_out * ny + L.cA;
+            if (!EDGE) {
+                if (L.wA) *reinterpret_cast<double2 *>(o) = v;
+            } else {
+                if (L.wA) o[0] = v.x;
+                if (L.wB) o[1] = v.y;
+            }
+        }
+    }
+}
+
+template <int K, bool EDGE>
+__device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, double *__restrict__ d,
+                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                                double coef) {
+    double2 X0[K], X1[K], X2[K], pf[3];
+#pragma unroll
+    for (int q = 0; q < K; ++q) X0[q] = X1[q] = X2[q] = make_double2(0.0, 0.0);
+    const int i0 = c0 - K, i1 = c1 + 2 * K - 1;
+    const int64_t ny = L.ny;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
+    int i = i0;
+    for (; i + 3 <= i1; i += 3) {
+        wt_iter<K, EDGE, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        wt_iter<K, EDGE, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        wt_iter<K, EDGE, 2>(X0, X1, X2, pf, s, d, g, L, i + 2, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    }
+    if (i < i1) wt_iter<K, EDGE, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    if (i + 1 < i1) wt_iter<K, EDGE, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ src, double *__restrict__ dst,
+                                                    const double *__restrict__ f0, int64_t field_stride, int ny,
+                                                    int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
+                                                    int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
+                                                    int n_fields, double coef, const double *__restrict__ minmax) {
+    constexpr int KH = K + (K & 1);           // even halo keeps 16-B alignment
+    constexpr int W = WT_COLS - 2 * KH;       // output columns per tile
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int lane = threadIdx.x & 63;
+    if (wave >= tiles_x * chunks_y * n_fields) return;
+    const int tx = wave % tiles_x;
+    const int ty = (wave / tiles_x) % chunks_y;
+    const int f = wave / (tiles_x * chunks_y);
+    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;  // uniform plane: zero delta
+    const int c0 = out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = tx * W;                    // first output column
+    WtLane L;
+    L.ny = ny;
+    L.cA = x0 - KH + 2 * lane;
+    const int cB = L.cA + 1;
+    L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
+    L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
+    L.lA = L.cA == 0;
+    L.rA = L.cA == ny - 1;
+    L.lB = cB == 0;
+    L.rB = cB == ny - 1;
+    const double *s = src + (int64_t)f * field_stride;
+    double *d = dst + (int64_t)f * field_stride;
+    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    // reflecting boundaries or ragged columns inside the tile -> EDGE body
+    const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
+                      (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
+                      (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
+    if (edge)
+        diffuse_wt_body<K, true>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    else
+        diffuse_wt_body<K, false>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+static int g_stencil_rows = 128;
+
+template <int K>
+static void launch_wt(hipStream_t st, const double *src, double *dst, const double *f0, int nf, int64_t fs,
+                      int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot, double coef,
+                      const double *mm) {
+    constexpr int KH = K + (K & 1);
+    constexpr int W = WT_COLS - 2 * KH;
+    const int rch = g_stencil_rows;
+    const int tiles_x = (ny + W - 1) / W;
+    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
+    const int waves = tiles_x * chunks_y * nf;
+    hipLaunchKernelGGL(k_diffuse_wt<K>, dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny, out_lo,
+                       out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+}
+
+static int g_stencil_kernel = 1;  // 0 = workgroup tile (LDS exchange), 1 = wave tile (DPP)
+
+static void launch_wt_k(int k, hipStream_t st, const double *src, double *dst, const double *f0, int nf,
+                        int64_t fs, int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot,
+                        double coef, const double *mm) {
+#define VK_WT(KC) case KC: launch_wt<KC>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm); break
+    switch (k) {
+        VK_WT(3); VK_WT(5); VK_WT(7); VK_WT(9); VK_WT(11); VK_WT(13); VK_WT(15);
+        default: break;
+    }
+#undef VK_WT
+}
+
+extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
+    const int prev = g_stencil_kernel;
+    if (variant == 0 || variant == 1) g_stencil_kernel = variant;
+    if (rows >= 8 && rows <= 4096) g_stencil_rows = rows;
+    return prev;
+}
+
+static int g_stencil_depth = 15;  // substeps per HBM pass (odd; 1 = one launch per substep)
+
+extern "C" int vk_set_stencil_depth(int32_t k) {
+    const int prev = g_stencil_depth;
+    if (k >= 1 && k <= 15) g_stencil_depth = k | 1;
+    return prev;
+}
+
+// rows [lo, hi) of every non-uniform plane: dst <- src
+__global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ src, double *__restrict__ dst,
+                                                   int64_t field_stride, int64_t off, int64_t count,
+                                                   const double *__restrict__ minmax) {
+    const int f = blockIdx.y;
+    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;
+    const int64_t base = (int64_t)f * field_stride + off;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x)
+        dst[base + i] = src[base + i];
+}
+
+template <int K>
+static void launch_tb(hipStream_t st, const double *src, double *dst, const double *f0, int nf,
+                      int64_t fs, int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot,
+                      double coef, const double *mm) {
+    const int rch = 128;
+    dim3 grid((ny + (TB_BX - 2 * K) - 1) / (TB_BX - 2 * K), (out_hi - out_lo + rch - 1) / rch, nf);
+    hipLaunchKernelGGL(k_diffuse_tb<K>, grid, dim3(TB_BX), 0, st, src, dst, f0, fs, ny, out_lo, out_hi, in_lo,
+                       in_hi, top, bot, rch, coef, mm);
+}
+
+static void launch_tb_k(int k, hipStream_t st, const double *src, double *dst, const double *f0, int nf,
+                        int64_t fs, int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot,
+                        double coef, const double *mm) {
+#define VK_TB(KC) case KC: launch_tb<KC>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm); break
+    switch (k) {  // odd depths only (see vk_diffuse)
+        VK_TB(3); VK_TB(5); VK_TB(7); VK_TB(9); VK_TB(11); VK_TB(13); VK_TB(15);
+        default: break;
+    }
+#undef VK_TB
+}
+
 extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                           int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
                           int32_t hi_max, int32_t edge_top, int32_t edge_bot, int32_t sub_begin,
@@ -81,38 +431,55 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         return VK_ERR_ARG;
     }
     if (n_fields == 0 || sub_count == 0) return VK_OK;
+    // The state after substep j lives in work[j & 1] (field after the last
+    // substep).  A pass of k substeps [j, j+k) reads work[(j-1)&1] (field for
+    // j == 0) and writes work[(j+k-1)&1]; k is kept ODD so the two differ.
     double *work[2] = {work0, work1};
     const int top_reflect = edge_top ? lo_min : -1;
     const int bot_reflect = edge_bot ? hi_max - 1 : 0x7fffffff;
     hipStream_t s = (hipStream_t)stream;
     const int last_in_call = sub_begin + sub_count - 1;
-    for (int jsub = sub_begin; jsub <= last_in_call; ++jsub) {
-        const int grow = last_in_call - jsub;
+    int depth = g_stencil_depth | 1;   // odd
+    if (depth > 15) depth = 15;
+    for (int j = sub_begin; j <= last_in_call;) {
+        int k = std::min(depth, last_in_call - j + 1);
+        if ((k & 1) == 0) k -= 1;   // even remainder: odd pass now, the rest next
+        const int e = j + k - 1;     // last substep of this pass
+        const int grow = last_in_call - e;
         const int lo = max(lo_min, row_lo - grow);
         const int hi = min(hi_max, row_hi + grow);
-        const double *src = (jsub == 0) ? field : work[(jsub - 1) & 1];
-        const bool final_sub = (jsub == n_sub - 1);
-        // a single-substep step cannot update `field` in place (neighbours
-        // would read new values): it goes through work0 and is copied back
-        const bool in_place = final_sub && jsub == 0;
-        double *dst = (final_sub && !in_place) ? field : work[jsub & 1];
-        const double *f0 = final_sub ? field : nullptr;
-        dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
-        hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo, hi,
-                           top_reflect, bot_reflect, coeff_dt, minmax);
-        if (in_place) {
-            int rc = vk::launch_check("k_diffuse_substep");
-            if (rc) return rc;
-            for (int f = 0; f < n_fields; ++f) {
-                const int64_t off = (int64_t)f * field_stride + (int64_t)row_lo * ny;
-                rc = vk::hip_check(hipMemcpyAsync(field + off, work0 + off,
-                                                  (size_t)(row_hi - row_lo) * ny * sizeof(double),
-                                                  hipMemcpyDeviceToDevice, s), "hipMemcpyAsync(diffuse)");
-                if (rc) return rc;
-            }
+        const int in_lo = max(lo_min, lo - k), in_hi = min(hi_max, hi + k);
+        const double *src = (j == 0) ? field : work[(j - 1) & 1];
+        const bool final_pass = (e == n_sub - 1);
+        // a pass that both starts from and ends in `field` cannot run in place
+        // (neighbours would read new values): it goes through work0 + copy
+        const bool in_place = final_pass && j == 0;
+        double *dst = (final_pass && !in_place) ? field : (in_place ? work0 : work[e & 1]);
+        const double *f0 = final_pass ? field : nullptr;
+        if (k == 1) {
+            dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
+            hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
+                               hi, top_reflect, bot_reflect, coeff_dt, minmax);
+        } else if (g_stencil_kernel == 1) {
+            launch_wt_k(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                        bot_reflect, coeff_dt, minmax);
+        } else {
+            launch_tb_k(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                        bot_reflect, coeff_dt, minmax);
         }
+        int rc = vk::launch_check("vk_diffuse kernel");
+        if (rc) return rc;
+        if (in_place) {
+            const int64_t count = (int64_t)(row_hi - row_lo) * ny;
+            const unsigned blocks = (unsigned)std::min<int64_t>(2048, (count + 255) / 256);
+            hipLaunchKernelGGL(k_copy_rows, dim3(blocks, n_fields), dim3(256), 0, s, work0, field, field_stride,
+                               (int64_t)row_lo * ny, count, minmax);
+            rc = vk::launch_check("k_copy_rows");
+            if (rc) return rc;
+        }
+        j += k;
     }
-    return vk::launch_check("k_diffuse_substep");
+    return VK_OK;
 }
 
 // ---------------------------------------------------------------------------

@@ -34,6 +34,18 @@ def n_substeps(timestep: float, dt_max: float = 0.01) -> int:
     return n
 
 
+def stencil_depth(k: int = 0) -> int:
+    """Set (1..15, odd) / query (0) the substeps fused per HBM pass; returns the previous."""
+    native.load()
+    return native._lib.vk_set_stencil_depth(int(k))
+
+
+def stencil_kernel(variant: int = -1, rows: int = 0) -> int:
+    """Select the fused-pass kernel (0 = workgroup/LDS, 1 = wave/DPP) and rows per tile."""
+    native.load()
+    return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
+
+
 class Lattice:
     def __init__(self, molecules: Sequence[str], n_bins, bounds, depth: float, diffusion: float,
                  device=None, row_band=None, halo: int = 0, avogadro: float = N_A_LEGACY,

@@ -211,19 +211,48 @@ def test_dopri5_status_and_limits(dev):
                    torch.ones(64, dtype=torch.float64, device=dev))
 
 
-def test_stencil_bitwise_vs_scipy_convolve(dev):
-    from lens_amd.lattice import Lattice
+@pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (1, 3), (1, 7), (1, 11), (1, 15)])
+def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
+    """Every kernel variant and temporal-blocking depth reproduces
+    scipy.ndimage.convolve bit for bit."""
+    from lens_amd.lattice import Lattice, stencil_depth, stencil_kernel
     z = np.load(os.path.join(GOLDEN, 'stencil.npz'))
-    for shape in ('17x23', '64x64', '128x96'):
-        f0 = z['f0_' + shape]
-        nx, ny = f0.shape
-        for dt in (1.0, 5.0, 10.0):
-            lat = Lattice(['a', 'b'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
-                          initial={'a': f0, 'b': np.full((nx, ny), 2.5)})
-            n_sub = lat.diffuse(dt)
-            assert n_sub == int(z['n_%s_dt%g' % (shape, dt)])
-            assert np.array_equal(lat.owned('a').cpu().numpy(), z['f_%s_dt%g' % (shape, dt)])
-            assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))  # uniform skip
+    prev = stencil_depth(depth)
+    prev_k = stencil_kernel(variant, 16)
+    try:
+        for shape in ('17x23', '64x64', '128x96'):
+            f0 = z['f0_' + shape]
+            nx, ny = f0.shape
+            for dt in (1.0, 5.0, 10.0):
+                lat = Lattice(['a', 'b'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                              initial={'a': f0, 'b': np.full((nx, ny), 2.5)})
+                n_sub = lat.diffuse(dt)
+                assert n_sub == int(z['n_%s_dt%g' % (shape, dt)])
+                assert np.array_equal(lat.owned('a').cpu().numpy(), z['f_%s_dt%g' % (shape, dt)]), (shape, dt)
+                assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))  # uniform skip
+    finally:
+        stencil_depth(prev)
+        stencil_kernel(prev_k, 128)
+
+
+@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
+def test_stencil_large_tiles_vs_c_oracle(dev, variant, shape):
+    """Multi-tile / multi-chunk geometry: interior tiles, ragged last tile and
+    chunk, odd widths."""
+    from lens_amd.lattice import Lattice, stencil_kernel
+    rng = np.random.default_rng(8)
+    nx, ny = shape
+    f0 = rng.random((nx, ny))
+    prev = stencil_kernel(variant, 64)
+    try:
+        lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+        lat.diffuse(1.0)
+    finally:
+        stencil_kernel(prev, 128)
+    ref = np.ascontiguousarray(f0.copy())
+    cpu.diffuse(ref, 5.0 * 0.01, 100)
+    assert np.array_equal(lat.owned('a').cpu().numpy(), ref)
 
 
 def test_single_substep_diffusion(dev):
