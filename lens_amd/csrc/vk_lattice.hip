@@ -199,19 +199,21 @@ __global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__
 
 constexpr int WT_COLS = 128;
 
+// bound_ctrl = true: the lane shifted in from outside the wave reads 0 (that
+// lane is tile halo), so no "old" operand has to be materialised.
 __device__ __forceinline__ double dpp_from_lane_below(double v) {  // lane l <- lane l-1
     int2 x = __builtin_bit_cast(int2, v);
     int2 y;
-    y.x = __builtin_amdgcn_update_dpp(0, x.x, 0x138, 0xf, 0xf, false);
-    y.y = __builtin_amdgcn_update_dpp(0, x.y, 0x138, 0xf, 0xf, false);
+    y.x = __builtin_amdgcn_mov_dpp(x.x, 0x138, 0xf, 0xf, true);
+    y.y = __builtin_amdgcn_mov_dpp(x.y, 0x138, 0xf, 0xf, true);
     return __builtin_bit_cast(double, y);
 }
 
 __device__ __forceinline__ double dpp_from_lane_above(double v) {  // lane l <- lane l+1
     int2 x = __builtin_bit_cast(int2, v);
     int2 y;
-    y.x = __builtin_amdgcn_update_dpp(0, x.x, 0x130, 0xf, 0xf, false);
-    y.y = __builtin_amdgcn_update_dpp(0, x.y, 0x130, 0xf, 0xf, false);
+    y.x = __builtin_amdgcn_mov_dpp(x.x, 0x130, 0xf, 0xf, true);
+    y.y = __builtin_amdgcn_mov_dpp(x.y, 0x130, 0xf, 0xf, true);
     return __builtin_bit_cast(double, y);
 }
 
@@ -229,7 +231,7 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
     return make_double2(p[row_off + a], p[row_off + b]);
 }
 
-template <int K, bool EDGE, int U>
+template <int K, bool EDGE, bool FINAL, int U>
 __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], double2 (&X2)[K], double2 (&pf)[3],
                                         const double *__restrict__ s, double *__restrict__ d,
                                         const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
@@ -243,9 +245,12 @@ __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], doub
     const int r_out = i - 2 * K + 1;
     const bool row_ok = r_out >= c0 && r_out < c1;
     double2 base = make_double2(0.0, 0.0);
-    if (g && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
+    if (FINAL && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
 #pragma unroll
     for (int q = K - 1; q >= 0; --q) {
+        // stage q only matters for output rows [c0-(K-1-q), c1+(K-1-q)):
+        // skip the pipeline fill/drain iterations (wave-uniform branch)
+        if (i < c0 - K + 3 * q + 2 || i > c1 + K - 1 + q) continue;
         const int r = i - 2 * q - 1;
         const double2 cen = CN[q];
         const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
@@ -264,7 +269,7 @@ __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], doub
         if (q + 1 < K) {
             UP[q + 1] = v;
         } else if (row_ok) {
-            if (g) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
             double *o = d + (int64_t)r_out * ny + L.cA;
             if (!EDGE) {
                 if (L.wA) *reinterpret_cast<double2 *>(o) = v;
@@ -276,7 +281,7 @@ __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], doub
     }
 }
 
-template <int K, bool EDGE>
+template <int K, bool EDGE, bool FINAL>
 __device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, double *__restrict__ d,
                                                 const double *__restrict__ g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
@@ -290,15 +295,15 @@ __device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, do
     for (int u = 0; u < 3; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
     int i = i0;
     for (; i + 3 <= i1; i += 3) {
-        wt_iter<K, EDGE, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-        wt_iter<K, EDGE, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-        wt_iter<K, EDGE, 2>(X0, X1, X2, pf, s, d, g, L, i + 2, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        wt_iter<K, EDGE, FINAL, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        wt_iter<K, EDGE, FINAL, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        wt_iter<K, EDGE, FINAL, 2>(X0, X1, X2, pf, s, d, g, L, i + 2, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
     }
-    if (i < i1) wt_iter<K, EDGE, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-    if (i + 1 < i1) wt_iter<K, EDGE, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    if (i < i1) wt_iter<K, EDGE, FINAL, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    if (i + 1 < i1) wt_iter<K, EDGE, FINAL, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
-template <int K>
+template <int K, bool FINAL>
 __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ src, double *__restrict__ dst,
                                                     const double *__restrict__ f0, int64_t field_stride, int ny,
                                                     int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
@@ -334,9 +339,9 @@ __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ s
                       (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
                       (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
     if (edge)
-        diffuse_wt_body<K, true>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        diffuse_wt_body<K, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
     else
-        diffuse_wt_body<K, false>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        diffuse_wt_body<K, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
 static int g_stencil_rows = 128;
@@ -351,8 +356,12 @@ static void launch_wt(hipStream_t st, const double *src, double *dst, const doub
     const int tiles_x = (ny + W - 1) / W;
     const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
-    hipLaunchKernelGGL(k_diffuse_wt<K>, dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny, out_lo,
-                       out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+    if (f0)
+        hipLaunchKernelGGL((k_diffuse_wt<K, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny,
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+    else
+        hipLaunchKernelGGL((k_diffuse_wt<K, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny,
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
 }
 
 static int g_stencil_kernel = 1;  // 0 = workgroup tile (LDS exchange), 1 = wave tile (DPP)

@@ -146,18 +146,24 @@ class Lattice:
         while j < n_sub:
             cnt = min(k, n_sub - j)
             if banded:
-                # substep j reads src(j): field for j == 0, else work[(j-1) & 1]
-                src = self.fields if j == 0 else (self.work0 if ((j - 1) & 1) == 0 else self.work1)
-                halo_exchange(src, cnt)
-            native.check(native._lib.vk_diffuse(
-                native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1),
-                len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, lo_min,
-                hi_max, int(self.edge_top), int(self.edge_bot), j, cnt, n_sub, coeff_dt,
-                native.ptr(mm), native.stream_handle()), 'vk_diffuse')
+                halo_exchange(self.state_buffer(j), cnt)
+            self._run_block(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max)
             j += cnt
         if events is not None:
             events[1].record()
         return n_sub
+
+    def state_buffer(self, j: int):
+        """Buffer holding the fields before substep j (vk_diffuse's rotation:
+        field for j == 0, else work[(j-1) & 1])."""
+        return self.fields if j == 0 else (self.work0 if ((j - 1) & 1) == 0 else self.work1)
+
+    def _run_block(self, j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max):
+        native.check(native._lib.vk_diffuse(
+            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1),
+            len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, lo_min,
+            hi_max, int(self.edge_top), int(self.edge_bot), j, cnt, n_sub, coeff_dt,
+            native.ptr(mm), native.stream_handle()), 'vk_diffuse')
 
     # -- agent coupling ------------------------------------------------------
     def bin_sites(self, loc, n_agents, bin_lin=None, ix=None):
