@@ -51,6 +51,10 @@ def parse():
     p.add_argument('--integrator', default='dopri5', choices=['dopri5', 'euler'])
     p.add_argument('--halo', type=int, default=10, help='halo depth = substeps per halo exchange')
     p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
+    p.add_argument('--generic-kernel', action='store_true',
+                   help='use the table-walking DP45 kernel instead of the specialised one')
+    p.add_argument('--stencil-depth', type=int, default=9)
+    p.add_argument('--stencil-rows', type=int, default=64)
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -77,11 +81,36 @@ def build_rank(args, rank, world, dev):
         n_local = n_total // world + (1 if rank < n_total % world else 0)
     params, conc = configs.heterogeneous_colony(table, cfg, n_local, seed=configs.SEED + rank)
     col = Colony(cfg, n_local, device=dev, integrator=args.integrator, environment=lat or 'held',
-                 table=table, exchange=args.exchange)
+                 table=table, exchange=args.exchange, specialize=not args.generic_kernel)
     col.set_agents(params=params, conc=conc, location=loc if nx else None)
     if nx:
         col.gather_external()
     return col, lat, (params, conc, loc if nx else None)
+
+
+def time_stencil_pass(lat, depth, reps=20):
+    """Average duration of ONE fused pass (k_diffuse_wt<depth>, non-final: fields ->
+    work buffer, fields untouched), HIP events on the launch stream."""
+    from lens_amd import native
+    lo_min = lat.row_lo if lat.edge_top else 0
+    hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
+    coeff = lat.diffusion * 0.01
+
+    def one():
+        native.check(native._lib.vk_diffuse(
+            native.ptr(lat.fields), native.ptr(lat.work0), native.ptr(lat.work1), len(lat.molecules),
+            lat.field_stride, lat.ny, lat.row_lo, lat.row_hi, lo_min, hi_max, int(lat.edge_top),
+            int(lat.edge_bot), 0, depth, 100, coeff, 0, native.stream_handle()), 'vk_diffuse')
+    for _ in range(3):
+        one()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        one()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
 
 
 def cpu_baseline(args, col, host_state):
@@ -138,6 +167,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
+    from lens_amd.lattice import stencil_depth, stencil_kernel
+    stencil_depth(args.stencil_depth)
+    stencil_kernel(1, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = None
     if world > 1 and lat is not None:
@@ -169,6 +201,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()
+    stencil_pass_ms = time_stencil_pass(lat, args.stencil_depth) if lat is not None else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(col.n)], dtype=torch.float64, device=dev)
     kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
@@ -185,7 +218,8 @@ def main():
     if rank == 0:
         n_total, nx, bound, desc = WORKLOADS[args.workload]
         integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
-        integ = {'kernel': 'k_dopri5_thread', 'avg_ms_per_step': kin_ms,
+        integ = {'kernel': 'vk_dopri5_spec' if col.engine.specialized else 'k_dopri5_thread',
+                 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / args.steps / col.n,
                  'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),
                  'achieved_tflops': integ_flops / (kin_ms * 1e-3) / 1e12 if kin_ms else None,
@@ -194,21 +228,27 @@ def main():
             integ['frac'] = integ['achieved_tflops'] / FP64_PEAK_TFLOPS
         roofline = None
         if lat is not None:
-            n_sub = n_substeps(1.0)
-            rows = lat.rows_local
+            # dominant kernel: one fused pass of `depth` substeps (k_diffuse_wt<depth>)
+            depth = args.stencil_depth
             cells = (lat.row_hi - lat.row_lo) * lat.ny * len(lat.molecules)
-            bytes_per_launch = 16.0 * cells
-            launch_ms = diff_ms / n_sub
+            launch_ms = stencil_pass_ms
+            bytes_per_launch = 16.0 * cells          # algorithmic: read + write each cell once
             achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
             traffic = None
-            pmc = os.path.join(REPO, 'profiles', 'pmc_diffuse.json')
+            pmc = os.path.join(REPO, 'profiles', 'pmc_stencil.json')
             if os.path.exists(pmc) and world == 1:
                 with open(pmc) as f:
-                    traffic = json.load(f).get('hbm_bytes_per_launch')
-            roofline = {'bound': 'hbm', 'kernel': 'k_diffuse_substep', 'achieved': achieved,
+                    rec = json.load(f)
+                if rec.get('kernel') == 'k_diffuse_wt<%d, false>' % depth and rec.get('cells') == cells:
+                    traffic = rec.get('hbm_bytes_per_launch')
+            roofline = {'bound': 'hbm', 'kernel': 'k_diffuse_wt<%d, false>' % depth, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
                         'traffic': traffic, 'bytes_per_launch': bytes_per_launch,
-                        'avg_launch_ms': launch_ms}
+                        'avg_launch_ms': launch_ms, 'substeps_per_launch': depth,
+                        'effective_stencil_gbps': bytes_per_launch * depth / (launch_ms * 1e-3) / 1e9,
+                        'fp64_tflops': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12,
+                        'fp64_frac': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                        'step_diffusion_ms': diff_ms}
         else:
             roofline = {'bound': 'fp64-valu', 'kernel': 'k_dopri5_thread',
                         'achieved': integ.get('achieved_tflops'), 'peak': FP64_PEAK_TFLOPS,

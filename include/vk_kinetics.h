@@ -107,7 +107,9 @@ typedef struct vk_ode_opts {
     double rtol;       /* relative tolerance (scipy RK45 semantics)          */
     double atol;       /* absolute tolerance                                 */
     int32_t max_steps; /* attempted steps per agent per call                 */
-    int32_t variant;   /* 0 = agent-per-thread                               */
+    int32_t variant;   /* 0 = agent-per-thread, table walked at run time;
+                          2 = agent-per-thread, network-specialised
+                              (vk_table_specialize)                          */
 } vk_ode_opts;
 
 int vk_abi_version(void);
@@ -115,6 +117,12 @@ const char *vk_last_error(void);
 
 int vk_table_create(const vk_table_desc *desc, vk_table **out);
 int vk_table_destroy(vk_table *table);
+
+/* Attach a network-specialised integrator to the table: `source` is the HIP
+ * source lens_amd/codegen.py generates from the same table (straight-line
+ * rate laws, every species/parameter/stage value in VGPRs); it is compiled
+ * with hiprtc for gfx950.  vk_step_dopri5 uses it for opts->variant == 2. */
+int vk_table_specialize(vk_table *table, const char *source);
 
 /* flux[r*ld + a] = sum over the reaction's rate laws (exact reference order). */
 int vk_rate_fluxes(const vk_table *t, int64_t n_agents, int64_t ld,

@@ -25,7 +25,7 @@ FLAGS = [
     '-ffp-contract=off',
     '-Wall', '-Wno-unused-function',
     '-I' + os.path.join(REPO, 'include'), '-I' + os.path.join(HERE, 'csrc'),
-    '-Wl,-rpath,/opt/rocm/lib',
+    '-Wl,-rpath,/opt/rocm/lib', '-lhiprtc',
 ]
 
 

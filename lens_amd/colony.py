@@ -43,7 +43,7 @@ class Colony:
                  integrator: str = 'dopri5', rtol: float = 1e-8, atol: float = 1e-12,
                  max_steps: int = 100000, environment='held', env_volume_L: float = 1e-14,
                  avogadro: float = N_A_LEGACY, exchange: str = 'sorted', mass_fg: float = 1339.0,
-                 table: Optional[RateLawTable] = None):
+                 table: Optional[RateLawTable] = None, specialize: bool = False):
         if integrator not in ('euler', 'dopri5'):
             raise ValueError('integrator must be euler or dopri5')
         if exchange not in ('sorted', 'atomic'):
@@ -52,6 +52,8 @@ class Colony:
         self.table = table or compile_rate_laws(config['reactions'], config['kinetic_parameters'])
         self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
         self.engine = KineticsEngine(self.table, self.device)
+        if specialize and integrator == 'dopri5':
+            self.engine.specialize()     # straight-line rate laws (hiprtc), bit-identical results
         self.n = int(n_agents)
         self.ld = int(capacity or n_agents)
         if self.n > self.ld:

@@ -23,6 +23,8 @@ struct vk_table {
     vk_dev_table dev;
     void *blob;  // single device allocation holding every array
     int32_t n_sets, n_members, n_upd, n_exch;
+    hipModule_t spec_module = nullptr;     // vk_table_specialize (hiprtc)
+    hipFunction_t spec_dopri5 = nullptr;
 };
 
 // Load through the constant address space: uniform index -> s_load (scalar cache).

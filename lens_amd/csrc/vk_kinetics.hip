@@ -21,6 +21,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <hip/hiprtc.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -157,9 +159,53 @@ extern "C" int vk_table_create(const vk_table_desc *d, vk_table **out) {
 
 extern "C" int vk_table_destroy(vk_table *t) {
     if (!t) return VK_OK;
+    if (t->spec_module) (void)hipModuleUnload(t->spec_module);
     int rc = vk::hip_check(hipFree(t->blob), "hipFree(table)");
     delete t;
     return rc;
+}
+
+// Compile a network-specialised integrator (source generated from this same
+// table by lens_amd/codegen.py) with hiprtc for gfx950 and attach it.
+extern "C" int vk_table_specialize(vk_table *t, const char *source) {
+    if (!t || !source) {
+        vk::set_error("vk_table_specialize: null argument");
+        return VK_ERR_ARG;
+    }
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, source, "vk_dopri5_spec.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        vk::set_error("vk_table_specialize: hiprtcCreateProgram failed");
+        return VK_ERR_HIP;
+    }
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    hiprtcResult cr = hiprtcCompileProgram(prog, 4, opts);
+    if (cr != HIPRTC_SUCCESS) {
+        size_t log_size = 0;
+        hiprtcGetProgramLogSize(prog, &log_size);
+        std::vector<char> log(log_size + 1, 0);
+        if (log_size) hiprtcGetProgramLog(prog, log.data());
+        vk::set_error("vk_table_specialize: compile failed: %.400s", log.data());
+        hiprtcDestroyProgram(&prog);
+        return VK_ERR_HIP;
+    }
+    size_t code_size = 0;
+    hiprtcGetCodeSize(prog, &code_size);
+    std::vector<char> code(code_size);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    hipModule_t mod;
+    int rc = vk::hip_check(hipModuleLoadData(&mod, code.data()), "hipModuleLoadData(spec)");
+    if (rc) return rc;
+    hipFunction_t fn;
+    rc = vk::hip_check(hipModuleGetFunction(&fn, mod, "vk_dopri5_spec"), "hipModuleGetFunction(spec)");
+    if (rc) {
+        (void)hipModuleUnload(mod);
+        return rc;
+    }
+    if (t->spec_module) (void)hipModuleUnload(t->spec_module);
+    t->spec_module = mod;
+    t->spec_dopri5 = fn;
+    return VK_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -590,6 +636,20 @@ extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double d
     if (!(dt > 0.0) || !(o->rtol > 0.0) || !(o->atol >= 0.0) || o->max_steps <= 0) {
         vk::set_error("vk_step_dopri5: need dt > 0, rtol > 0, atol >= 0, max_steps > 0");
         return VK_ERR_ARG;
+    }
+    if (o->variant == 2) {  // network-specialised kernel (vk_table_specialize)
+        if (!t->spec_dopri5) {
+            vk::set_error("vk_step_dopri5: variant 2 needs vk_table_specialize first");
+            return VK_ERR_ARG;
+        }
+        double rtol = o->rtol, atol = o->atol;
+        int max_steps = o->max_steps;
+        void *args[] = {&n, &ld, &dt, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c,
+                        &delta, &h_state, &flux, &counts, &status, &nsteps};
+        const unsigned blocks = (unsigned)((n + 255) / 256);
+        return vk::hip_check(hipModuleLaunchKernel(t->spec_dopri5, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream,
+                                                   args, nullptr),
+                             "hipModuleLaunchKernel(vk_dopri5_spec)");
     }
     if (o->variant != 0) {
         vk::set_error("vk_step_dopri5: variant %d not available", o->variant);

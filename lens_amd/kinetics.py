@@ -40,6 +40,19 @@ class KineticsEngine:
         self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
         with torch.cuda.device(self.device):
             self.dev = native.DeviceTable(table)
+        self.specialized = False
+
+    def specialize(self):
+        """Compile the network-specialised DP45 kernel (hiprtc) for this table.
+
+        Afterwards :meth:`dopri5` defaults to variant 2 (straight-line rate
+        laws, everything in VGPRs) instead of the generic table walk."""
+        from lens_amd.codegen import dopri5_source
+        with torch.cuda.device(self.device):
+            native.check(native._lib.vk_table_specialize(self.dev.handle, dopri5_source(self.table).encode()),
+                         'vk_table_specialize')
+        self.specialized = True
+        return self
 
     # -- allocation helpers -------------------------------------------------
     def empty_like_agents(self, rows, ld, dtype=F64):
@@ -93,11 +106,15 @@ class KineticsEngine:
 
     def dopri5(self, dt, params, conc, mmol_to_counts, n_agents=None, h_state=None, rtol=1e-8,
                atol=1e-12, max_steps=100000, flux=None, counts=None, status=None, nsteps=None,
-               variant=0, delta=None):
+               variant=None, delta=None):
         """Adaptive DP5(4) over [0, dt] in place on ``conc``.
 
-        Returns (flux = mean flux over dt, counts, status, nsteps)."""
+        ``variant``: 0 = generic table walk, 2 = network-specialised (default
+        once :meth:`specialize` ran).  Returns (flux = mean flux over dt,
+        counts, status, nsteps)."""
         t = self.table
+        if variant is None:
+            variant = 2 if self.specialized else 0
         n = conc.shape[1] if n_agents is None else n_agents
         ld = self._check_state(params, conc, n)
         _need(mmol_to_counts, 'mmol_to_counts', None, ld, F64, self.device)

@@ -25,7 +25,7 @@ VK_AGENT_MAX_STEPS, VK_AGENT_H_UNDERFLOW, VK_AGENT_NONFINITE = 1, 2, 4
 
 # every symbol include/vk_kinetics.h declares (tests check the exports)
 EXPORTS = (
-    'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy',
+    'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy', 'vk_table_specialize',
     'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_field_minmax',
     'vk_diffuse', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites',
@@ -65,6 +65,7 @@ _SIGS = {
     'vk_last_error': ([], ctypes.c_char_p),
     'vk_table_create': ([ctypes.POINTER(VkTableDesc), ctypes.POINTER(_vp)], ctypes.c_int),
     'vk_table_destroy': ([_vp], ctypes.c_int),
+    'vk_table_specialize': ([_vp, ctypes.c_char_p], ctypes.c_int),
     'vk_rate_fluxes': ([_vp, _i64, _i64, _vp, _vp, _vp, _vp], ctypes.c_int),
     'vk_step_euler': ([_vp, _i64, _i64, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     'vk_step_dopri5': ([_vp, _i64, _i64, _f64, ctypes.POINTER(VkOdeOpts), _vp, _vp, _vp, _vp,

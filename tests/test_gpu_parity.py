@@ -387,3 +387,24 @@ def test_process_drop_in_update_dict(dev):
         fl, deltas, counts = agent.next_update(1.0, st, 733058.77)
         assert got['fluxes'] == fl and got['internal'] == deltas['internal']
         assert {m: v['_value'] for m, v in got['fields'].items()} == counts
+
+
+@pytest.mark.parametrize('name', ['glc_lct', 'glc_ac', 'glc_lct_transport'])
+def test_specialized_dopri5_bitwise_equals_generic(dev, name):
+    """The hiprtc-specialised kernel evaluates the same operations in the same
+    order as the table-walking kernel: identical end states and step counts."""
+    cfg = {'glc_lct': configs.glc_lct_config, 'glc_ac': configs.glc_ac_config,
+           'glc_lct_transport': configs.glc_lct_transport_config}[name]()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    n = 3000
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=12)
+    m2c = torch.full((n,), mmol_to_counts(), dtype=torch.float64, device=dev)
+    eng = _engine(t, dev)
+    p = torch.from_numpy(params).to(dev)
+    c0 = torch.from_numpy(conc.copy()).to(dev)
+    c2 = torch.from_numpy(conc.copy()).to(dev)
+    f0, k0, s0, n0 = eng.dopri5(1.0, p, c0, m2c, variant=0)
+    eng.specialize()
+    f2, k2, s2, n2 = eng.dopri5(1.0, p, c2, m2c)
+    assert torch.equal(c0, c2) and torch.equal(f0, f2) and torch.equal(k0, k2)
+    assert torch.equal(n0, n2) and torch.equal(s0, s2)
