@@ -173,9 +173,9 @@ def main():
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = None
     if world > 1 and lat is not None:
-        from lens_amd.distributed import make_halo_exchange, make_minmax_allreduce
+        from lens_amd.distributed import make_halo_exchange, make_uniform_allreduce
         halo_ex = make_halo_exchange(lat, rank, world)
-        allred = make_minmax_allreduce()
+        allred = make_uniform_allreduce()
 
     def barrier():
         if dist is not None:

@@ -23,7 +23,7 @@
  *       (vivarium/processes/Kremling2007_transport.py:384) for convenience
  *       networks: adaptive Dormand-Prince 5(4) over [0, dt] on the augmented
  *       system (internal species + per-reaction flux integrals).
- *   vk_field_minmax + vk_diffuse
+ *   vk_field_uniform + vk_diffuse
  *       replace DiffusionField.diffuse / diffusion_delta
  *       (vivarium/processes/diffusion_field.py:385-407): fixed dt=0.01
  *       substeps of the reflect-boundary 5-point Laplacian, uniform-field skip.
@@ -153,10 +153,14 @@ int vk_step_dopri5(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
 /* Lattice fields: n_fields planes of rows x ny doubles, plane stride
  * field_stride.  Local rows may include halo rows of neighbouring ranks.   */
 
-/* minmax[2f] = min, minmax[2f+1] = max over rows [row_lo, row_hi). */
-int vk_field_minmax(const double *fields, int32_t n_fields, int64_t field_stride,
-                    int32_t ny, int32_t row_lo, int32_t row_hi, double *minmax,
-                    vk_stream_t stream);
+/* Uniform-plane test over rows [row_lo, row_hi) (diffusion_field.py:401-404).
+ * summary[2f] == summary[2f+1] iff plane f holds a single value (both then
+ * hold it); otherwise summary = (-inf, +inf) (a NaN plane is non-uniform).
+ * Element-wise min of [2f] / max of [2f+1] over ranks gives the global test.
+ * Early exit: cost is ~O(1) for a non-uniform plane.                       */
+int vk_field_uniform(const double *fields, int32_t n_fields, int64_t field_stride,
+                     int32_t ny, int32_t row_lo, int32_t row_hi, double *summary,
+                     vk_stream_t stream);
 
 /* Substeps [sub_begin, sub_begin+sub_count) of an n_sub-substep diffusion.
  * Substep j reads src(j) and writes dst(j):
@@ -166,12 +170,13 @@ int vk_field_minmax(const double *fields, int32_t n_fields, int64_t field_stride
  * [max(lo_min, row_lo-g), min(hi_max, row_hi+g)) with
  * g = sub_begin+sub_count-1-j (halo shrinking); rows lo_min and hi_max-1 are
  * reflected (Neumann) if they are global edges (edge_top/edge_bot != 0).
- * coeff_dt = (D/(dx*dy)) * 0.01.  minmax (nullable) skips uniform fields.  */
+ * coeff_dt = (D/(dx*dy)) * 0.01.  uniform (nullable, a vk_field_uniform summary)
+ * skips uniform planes.                                                      */
 int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi,
                int32_t lo_min, int32_t hi_max, int32_t edge_top, int32_t edge_bot,
                int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
-               const double *minmax, vk_stream_t stream);
+               const double *uniform, vk_stream_t stream);
 
 /* Substeps fused per HBM pass by vk_diffuse (temporal blocking; odd, 1..15;
  * 1 = one launch per substep).  Returns the previous value; k outside 1..15

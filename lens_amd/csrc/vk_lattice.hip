@@ -33,9 +33,9 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
                                                            const double *__restrict__ f0,
                                                            int64_t field_stride, int ny, int lo, int hi,
                                                            int top_reflect, int bot_reflect, double coef,
-                                                           const double *__restrict__ minmax) {
+                                                           const double *__restrict__ uniform) {
     const int f = blockIdx.z;
-    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;  // uniform: delta is zero
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform: delta is zero
     const int j = blockIdx.x * ST_BX + threadIdx.x;
     const int r0 = lo + blockIdx.y * ST_RB;
     if (j >= ny || r0 >= hi) return;
@@ -167,9 +167,9 @@ __global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__
                                                       const double *__restrict__ f0, int64_t field_stride, int ny,
                                                       int out_lo, int out_hi, int in_lo, int in_hi,
                                                       int top_reflect, int bot_reflect, int rows_per_chunk,
-                                                      double coef, const double *__restrict__ minmax) {
+                                                      double coef, const double *__restrict__ uniform) {
     const int f = blockIdx.z;
-    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;  // uniform plane: zero delta
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform plane: zero delta
     const int c0 = out_lo + blockIdx.y * rows_per_chunk;
     if (c0 >= out_hi) return;
     const int c1 = min(c0 + rows_per_chunk, out_hi);
@@ -231,7 +231,9 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
     return make_double2(p[row_off + a], p[row_off + b]);
 }
 
-template <int K, bool EDGE, bool FINAL, int U>
+// STEADY: every stage is inside its useful row range (no fill/drain test),
+// so the K stages are straight-line code the scheduler can interleave.
+template <int K, bool EDGE, bool FINAL, bool STEADY, int U>
 __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], double2 (&X2)[K], double2 (&pf)[3],
                                         const double *__restrict__ s, double *__restrict__ d,
                                         const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
@@ -243,14 +245,14 @@ __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], doub
     NW[0] = pf[U];                                                                   // row i
     pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny, L);  // prefetch row i+3
     const int r_out = i - 2 * K + 1;
-    const bool row_ok = r_out >= c0 && r_out < c1;
+    const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
     double2 base = make_double2(0.0, 0.0);
     if (FINAL && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
 #pragma unroll
     for (int q = K - 1; q >= 0; --q) {
         // stage q only matters for output rows [c0-(K-1-q), c1+(K-1-q)):
         // skip the pipeline fill/drain iterations (wave-uniform branch)
-        if (i < c0 - K + 3 * q + 2 || i > c1 + K - 1 + q) continue;
+        if (!STEADY && (i < c0 - K + 3 * q + 2 || i > c1 + K - 1 + q)) continue;
         const int r = i - 2 * q - 1;
         const double2 cen = CN[q];
         const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
@@ -293,14 +295,22 @@ __device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, do
     const int64_t ny = L.ny;
 #pragma unroll
     for (int u = 0; u < 3; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
+    // iterations [s_lo, s_hi] have every stage active (fill ends, drain not begun)
+    const int s_lo = c0 + 2 * K - 1, s_hi = c1 + K - 1;
+#define WT_RUN(ST, U, I) wt_iter<K, EDGE, FINAL, ST, U>(X0, X1, X2, pf, s, d, g, L, I, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef)
     int i = i0;
-    for (; i + 3 <= i1; i += 3) {
-        wt_iter<K, EDGE, FINAL, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-        wt_iter<K, EDGE, FINAL, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-        wt_iter<K, EDGE, FINAL, 2>(X0, X1, X2, pf, s, d, g, L, i + 2, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    for (; i + 3 <= i1 && i < s_lo; i += 3) {   // fill
+        WT_RUN(false, 0, i); WT_RUN(false, 1, i + 1); WT_RUN(false, 2, i + 2);
     }
-    if (i < i1) wt_iter<K, EDGE, FINAL, 0>(X0, X1, X2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-    if (i + 1 < i1) wt_iter<K, EDGE, FINAL, 1>(X0, X1, X2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    for (; i + 2 <= s_hi; i += 3) {              // steady state: branch-free stages
+        WT_RUN(true, 0, i); WT_RUN(true, 1, i + 1); WT_RUN(true, 2, i + 2);
+    }
+    for (; i + 3 <= i1; i += 3) {                // drain
+        WT_RUN(false, 0, i); WT_RUN(false, 1, i + 1); WT_RUN(false, 2, i + 2);
+    }
+    if (i < i1) WT_RUN(false, 0, i);
+    if (i + 1 < i1) WT_RUN(false, 1, i + 1);
+#undef WT_RUN
 }
 
 template <int K, bool FINAL>
@@ -308,7 +318,7 @@ __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ s
                                                     const double *__restrict__ f0, int64_t field_stride, int ny,
                                                     int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
                                                     int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
-                                                    int n_fields, double coef, const double *__restrict__ minmax) {
+                                                    int n_fields, double coef, const double *__restrict__ uniform) {
     constexpr int KH = K + (K & 1);           // even halo keeps 16-B alignment
     constexpr int W = WT_COLS - 2 * KH;       // output columns per tile
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
@@ -317,7 +327,7 @@ __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ s
     const int tx = wave % tiles_x;
     const int ty = (wave / tiles_x) % chunks_y;
     const int f = wave / (tiles_x * chunks_y);
-    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;  // uniform plane: zero delta
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform plane: zero delta
     const int c0 = out_lo + ty * rows_per_chunk;
     const int c1 = min(c0 + rows_per_chunk, out_hi);
     const int x0 = tx * W;                    // first output column
@@ -395,9 +405,9 @@ extern "C" int vk_set_stencil_depth(int32_t k) {
 // rows [lo, hi) of every non-uniform plane: dst <- src
 __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ src, double *__restrict__ dst,
                                                    int64_t field_stride, int64_t off, int64_t count,
-                                                   const double *__restrict__ minmax) {
+                                                   const double *__restrict__ uniform) {
     const int f = blockIdx.y;
-    if (minmax && minmax[2 * f] == minmax[2 * f + 1]) return;
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;
     const int64_t base = (int64_t)f * field_stride + off;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x)
         dst[base + i] = src[base + i];
@@ -427,7 +437,7 @@ static void launch_tb_k(int k, hipStream_t st, const double *src, double *dst, c
 extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                           int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
                           int32_t hi_max, int32_t edge_top, int32_t edge_bot, int32_t sub_begin,
-                          int32_t sub_count, int32_t n_sub, double coeff_dt, const double *minmax,
+                          int32_t sub_count, int32_t n_sub, double coeff_dt, const double *uniform,
                           vk_stream_t stream) {
     if (!field || n_fields < 0 || ny <= 0 || row_lo < lo_min || row_hi > hi_max || row_lo >= row_hi ||
         sub_begin < 0 || sub_count < 0 || sub_begin + sub_count > n_sub ||
@@ -468,13 +478,13 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         if (k == 1) {
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
-                               hi, top_reflect, bot_reflect, coeff_dt, minmax);
+                               hi, top_reflect, bot_reflect, coeff_dt, uniform);
         } else if (g_stencil_kernel == 1) {
             launch_wt_k(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
-                        bot_reflect, coeff_dt, minmax);
+                        bot_reflect, coeff_dt, uniform);
         } else {
             launch_tb_k(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
-                        bot_reflect, coeff_dt, minmax);
+                        bot_reflect, coeff_dt, uniform);
         }
         int rc = vk::launch_check("vk_diffuse kernel");
         if (rc) return rc;
@@ -482,7 +492,7 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             const int64_t count = (int64_t)(row_hi - row_lo) * ny;
             const unsigned blocks = (unsigned)std::min<int64_t>(2048, (count + 255) / 256);
             hipLaunchKernelGGL(k_copy_rows, dim3(blocks, n_fields), dim3(256), 0, s, work0, field, field_stride,
-                               (int64_t)row_lo * ny, count, minmax);
+                               (int64_t)row_lo * ny, count, uniform);
             rc = vk::launch_check("k_copy_rows");
             if (rc) return rc;
         }
@@ -492,67 +502,65 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
 }
 
 // ---------------------------------------------------------------------------
-// min / max per plane (uniform-field test; multi-rank callers all-reduce)
+// uniform-plane test (diffusion_field.py:401-404: a field whose values are all
+// equal gets a zero delta).  Summary per plane: sum[2f] == sum[2f+1] iff the
+// owned rows hold one value (both = that value); otherwise (-inf, +inf).  The
+// summary min/max-reduces across ranks (distributed.make_uniform_allreduce).
+// A non-uniform plane is detected by the first blocks that run; every later
+// block reads the summary once and exits, so the common case costs a few
+// microseconds instead of a full read of the plane.
 // ---------------------------------------------------------------------------
 
-__global__ void k_minmax_init(double *mm, int n_fields) {
-    const int i = threadIdx.x;
-    if (i < n_fields) {
-        mm[2 * i] = INFINITY;
-        mm[2 * i + 1] = -INFINITY;
+__global__ void k_uniform_init(const double *__restrict__ fields, int64_t field_stride, int64_t off,
+                               int n_fields, double *sum) {
+    const int f = threadIdx.x;
+    if (f < n_fields) {
+        const double v0 = fields[(int64_t)f * field_stride + off];
+        const bool nan = !(v0 == v0);   // NaN != NaN: a NaN plane is non-uniform
+        sum[2 * f] = nan ? -INFINITY : v0;
+        sum[2 * f + 1] = nan ? INFINITY : v0;
     }
 }
 
-__global__ __launch_bounds__(256) void k_minmax(const double *__restrict__ fields, int64_t field_stride,
-                                                int64_t off, int64_t count, double *mm) {
+constexpr int UN_PER_THREAD = 8;
+
+__global__ __launch_bounds__(256) void k_uniform_probe(const double *__restrict__ fields, int64_t field_stride,
+                                                       int64_t off, int64_t count, double *sum) {
     const int f = blockIdx.y;
+    volatile double *vs = sum + 2 * f;
+    const double v0 = vs[0];
+    if (!(v0 == vs[1])) return;                       // already non-uniform (or NaN)
     const double *p = fields + (int64_t)f * field_stride + off;
-    double lo = INFINITY, hi = -INFINITY;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const double v = p[i];
-        lo = fmin(lo, v);
-        hi = fmax(hi, v);
-    }
+    const int64_t base = (int64_t)blockIdx.x * (256 * UN_PER_THREAD) + threadIdx.x;
+    bool diff = false;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        lo = fmin(lo, __shfl_xor(lo, o));
-        hi = fmax(hi, __shfl_xor(hi, o));
+    for (int k = 0; k < UN_PER_THREAD; ++k) {
+        const int64_t i = base + (int64_t)k * 256;
+        if (i < count) diff |= !(p[i] == v0);
     }
-    __shared__ double slo[4], shi[4];
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        slo[w] = lo;
-        shi[w] = hi;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int k = 1; k < (int)(blockDim.x >> 6); ++k) {
-            lo = fmin(lo, slo[k]);
-            hi = fmax(hi, shi[k]);
-        }
-        __hip_atomic_fetch_min(&mm[2 * f], lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_max(&mm[2 * f + 1], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__syncthreads_or(diff) && threadIdx.x == 0) {
+        vs[0] = -INFINITY;
+        vs[1] = INFINITY;
     }
 }
 
-extern "C" int vk_field_minmax(const double *fields, int32_t n_fields, int64_t field_stride, int32_t ny,
-                               int32_t row_lo, int32_t row_hi, double *minmax, vk_stream_t stream) {
-    if (!fields || !minmax || n_fields < 0 || n_fields > 1024 || ny <= 0 || row_lo < 0 || row_hi < row_lo ||
+extern "C" int vk_field_uniform(const double *fields, int32_t n_fields, int64_t field_stride, int32_t ny,
+                                int32_t row_lo, int32_t row_hi, double *summary, vk_stream_t stream) {
+    if (!fields || !summary || n_fields < 0 || n_fields > 1024 || ny <= 0 || row_lo < 0 || row_hi <= row_lo ||
         (int64_t)row_hi * ny > field_stride) {
-        vk::set_error("vk_field_minmax: bad arguments");
+        vk::set_error("vk_field_uniform: bad arguments");
         return VK_ERR_ARG;
     }
     if (n_fields == 0) return VK_OK;
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(k_minmax_init, dim3(1), dim3(1024), 0, s, minmax, n_fields);
+    const int64_t off = (int64_t)row_lo * ny;
+    hipLaunchKernelGGL(k_uniform_init, dim3(1), dim3(1024), 0, s, fields, field_stride, off, n_fields, summary);
     const int64_t count = (int64_t)(row_hi - row_lo) * ny;
-    if (count > 0) {
-        const unsigned blocks = (unsigned)std::min<int64_t>(1024, (count + 255) / 256);
-        hipLaunchKernelGGL(k_minmax, dim3(blocks, n_fields), dim3(256), 0, s, fields, field_stride,
-                           (int64_t)row_lo * ny, count, minmax);
-    }
-    return vk::launch_check("k_minmax");
+    const int64_t per_block = 256 * UN_PER_THREAD;
+    const unsigned blocks = (unsigned)((count + per_block - 1) / per_block);
+    hipLaunchKernelGGL(k_uniform_probe, dim3(blocks, n_fields), dim3(256), 0, s, fields, field_stride, off, count,
+                       summary);
+    return vk::launch_check("k_uniform_probe");
 }
 
 // ---------------------------------------------------------------------------

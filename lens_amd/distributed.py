@@ -63,8 +63,10 @@ def make_halo_exchange(lat, rank: int, world: int, group=None):
     return exchange
 
 
-def make_minmax_allreduce(group=None):
-    """minmax = [min0, max0, min1, max1, ...] -> global min / max (one all-reduce)."""
+def make_uniform_allreduce(group=None):
+    """Uniformity summary [lo0, hi0, lo1, hi1, ...] (vk_field_uniform) -> element-wise
+    min of the lo entries and max of the hi entries over ranks (one all-reduce):
+    lo == hi afterwards iff every rank's band holds the same single value."""
 
     def allreduce(mm):
         mm[0::2].neg_()

@@ -82,7 +82,7 @@ class Lattice:
         self.fields = torch.zeros(shape, dtype=torch.float64, device=self.device)
         self.work0 = torch.empty(shape, dtype=torch.float64, device=self.device)
         self.work1 = torch.empty(shape, dtype=torch.float64, device=self.device)
-        self.minmax = torch.empty(2 * max(nf, 1), dtype=torch.float64, device=self.device)
+        self.uniform = torch.empty(2 * max(nf, 1), dtype=torch.float64, device=self.device)
         if initial is not None:
             for f, m in enumerate(self.molecules):
                 if m in initial:
@@ -117,13 +117,15 @@ class Lattice:
         return sl if molecule is None else sl[self.molecules.index(molecule)]
 
     # -- diffusion ------------------------------------------------------------
-    def uniform_minmax(self, allreduce: Optional[Callable] = None):
-        native.check(native._lib.vk_field_minmax(
+    def uniform_summary(self, allreduce: Optional[Callable] = None):
+        """Per-plane uniformity summary (vk_field_uniform): [2f] == [2f+1] iff plane f
+        holds one value; ``allreduce`` (multi-rank) makes it the global test."""
+        native.check(native._lib.vk_field_uniform(
             native.ptr(self.fields), len(self.molecules), self.field_stride, self.ny, self.row_lo,
-            self.row_hi, native.ptr(self.minmax), native.stream_handle()), 'vk_field_minmax')
+            self.row_hi, native.ptr(self.uniform), native.stream_handle()), 'vk_field_uniform')
         if allreduce is not None:
-            allreduce(self.minmax)
-        return self.minmax
+            allreduce(self.uniform)
+        return self.uniform
 
     def diffuse(self, timestep: float, halo_exchange: Optional[Callable] = None,
                 allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None):
@@ -133,7 +135,7 @@ class Lattice:
         stream around the substep kernels only (bench roofline timing)."""
         n_sub = n_substeps(timestep, self.diffusion_dt)
         coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
-        mm = self.uniform_minmax(allreduce) if skip_uniform else None
+        mm = self.uniform_summary(allreduce) if skip_uniform else None
         if events is not None:
             events[0].record()
         banded = bool(self.pad_top or self.pad_bot)

@@ -26,7 +26,7 @@ VK_AGENT_MAX_STEPS, VK_AGENT_H_UNDERFLOW, VK_AGENT_NONFINITE = 1, 2, 4
 # every symbol include/vk_kinetics.h declares (tests check the exports)
 EXPORTS = (
     'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy', 'vk_table_specialize',
-    'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_field_minmax',
+    'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_field_uniform',
     'vk_diffuse', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites',
 )
@@ -70,7 +70,7 @@ _SIGS = {
     'vk_step_euler': ([_vp, _i64, _i64, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     'vk_step_dopri5': ([_vp, _i64, _i64, _f64, ctypes.POINTER(VkOdeOpts), _vp, _vp, _vp, _vp,
                         _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
-    'vk_field_minmax': ([_vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
+    'vk_field_uniform': ([_vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
     'vk_diffuse': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                     _i32, _i32, _i32, _f64, _vp, _vp], ctypes.c_int),
     'vk_set_stencil_depth': ([_i32], ctypes.c_int),

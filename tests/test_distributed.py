@@ -17,7 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from lens_amd.distributed import row_bands, make_halo_exchange, make_minmax_allreduce
+from lens_amd.distributed import row_bands, make_halo_exchange, make_uniform_allreduce
 from lens_amd.lattice import Lattice
 from oracle import lattice as olat
 
@@ -72,16 +72,22 @@ def _worker(rank, world, port, halo, f0, result_q):
                       row_band=band, halo=halo, initial={'a': f0, 'u': np.full((nx, ny), 4.0)})
         lat._run_block = lambda *a: cpu_run_block(lat, *a)
 
-        def minmax(allreduce=None):
+        def uniform(allreduce=None):
+            # CPU stand-in for vk_field_uniform's summary: (v, v) or (-inf, +inf)
             own = lat.fields[:, lat.row_lo:lat.row_hi]
-            mm = torch.stack([own.amin(dim=(1, 2)), own.amax(dim=(1, 2))], 1).flatten().contiguous()
+            rows = []
+            for f in range(own.shape[0]):
+                v0 = own[f].flatten()[0]
+                uni = bool((own[f] == v0).all())
+                rows.append([v0, v0] if uni else [-float('inf'), float('inf')])
+            mm = torch.tensor(rows, dtype=torch.float64).flatten().contiguous()
             if allreduce is not None:
                 allreduce(mm)
-            lat.minmax = mm
+            lat.uniform = mm
             return mm
-        lat.uniform_minmax = minmax
+        lat.uniform_summary = uniform
         lat.diffuse(1.0, halo_exchange=make_halo_exchange(lat, rank, world),
-                    allreduce=make_minmax_allreduce())
+                    allreduce=make_uniform_allreduce())
         result_q.put((rank, band, lat.owned().numpy().copy()))
     finally:
         dist.barrier()

@@ -235,24 +235,58 @@ def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
         stencil_kernel(prev_k, 128)
 
 
-@pytest.mark.parametrize('variant', [0, 1])
+@pytest.mark.parametrize('variant,depth,rows', [(0, 15, 64), (1, 15, 64), (1, 5, 256), (1, 9, 128),
+                                                (1, 13, 32), (1, 7, 512)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
-def test_stencil_large_tiles_vs_c_oracle(dev, variant, shape):
+def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
     """Multi-tile / multi-chunk geometry: interior tiles, ragged last tile and
-    chunk, odd widths."""
-    from lens_amd.lattice import Lattice, stencil_kernel
+    chunk, odd widths; pipeline fill / branch-free steady state / drain."""
+    from lens_amd.lattice import Lattice, stencil_depth, stencil_kernel
     rng = np.random.default_rng(8)
     nx, ny = shape
     f0 = rng.random((nx, ny))
-    prev = stencil_kernel(variant, 64)
+    prev = stencil_kernel(variant, rows)
+    prev_d = stencil_depth(depth)
     try:
         lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
         lat.diffuse(1.0)
     finally:
         stencil_kernel(prev, 128)
+        stencil_depth(prev_d)
     ref = np.ascontiguousarray(f0.copy())
     cpu.diffuse(ref, 5.0 * 0.01, 100)
     assert np.array_equal(lat.owned('a').cpu().numpy(), ref)
+
+
+def test_uniform_summary(dev):
+    """vk_field_uniform: (v, v) for a one-valued plane, (-inf, inf) otherwise --
+    including a single differing cell at the very end and a NaN plane."""
+    from lens_amd.lattice import Lattice
+    nx, ny = 300, 257
+    planes = {'u': np.full((nx, ny), 3.25), 'z': np.zeros((nx, ny)), 'last': np.full((nx, ny), 1.0),
+              'first': np.full((nx, ny), 1.0), 'nan': np.full((nx, ny), np.nan),
+              'inf': np.full((nx, ny), np.inf), 'rnd': np.random.default_rng(1).random((nx, ny))}
+    planes['last'][-1, -1] = 1.0 + 2 ** -52
+    planes['first'][0, 0] = -0.0 + 2.0
+    lat = Lattice(list(planes), (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial=planes)
+    got = lat.uniform_summary().cpu().numpy().reshape(-1, 2)
+    expect = {'u': (3.25, 3.25), 'z': (0.0, 0.0), 'inf': (np.inf, np.inf)}
+    for f, name in enumerate(planes):
+        lo, hi = got[f]
+        if name in expect:
+            assert (lo, hi) == expect[name], name
+        else:
+            assert lo == -np.inf and hi == np.inf, name
+    # uniform planes come through a diffusion step unchanged, non-uniform ones move
+    before = lat.owned().cpu().numpy().copy()
+    lat.diffuse(1.0)
+    after = lat.owned().cpu().numpy()
+    for f, name in enumerate(planes):
+        if name in ('u', 'z', 'inf'):
+            assert np.array_equal(after[f], before[f]), name
+    ref = np.ascontiguousarray(planes['rnd'].copy())
+    cpu.diffuse(ref, 5.0 * 0.01, 100)
+    assert np.array_equal(after[list(planes).index('rnd')], ref)
 
 
 def test_single_substep_diffusion(dev):
