@@ -239,7 +239,8 @@ def main():
             if os.path.exists(pmc) and world == 1:
                 with open(pmc) as f:
                     rec = json.load(f)
-                if rec.get('kernel') == 'k_diffuse_wt<%d, false>' % depth and rec.get('cells') == cells:
+                # the committed PMC pass must describe this exact launch geometry
+                if (rec.get('depth'), rec.get('rows'), rec.get('cells')) == (depth, args.stencil_rows, cells):
                     traffic = rec.get('hbm_bytes_per_launch')
             roofline = {'bound': 'hbm', 'kernel': 'k_diffuse_wt<%d, false>' % depth, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
