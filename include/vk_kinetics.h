@@ -107,7 +107,11 @@ typedef struct vk_ode_opts {
     double rtol;       /* relative tolerance (scipy RK45 semantics)          */
     double atol;       /* absolute tolerance                                 */
     int32_t max_steps; /* attempted steps per agent per call                 */
-    int32_t variant;   /* 0 = agent-per-thread, table walked at run time;
+    int32_t variant;   /* 0 = agent-per-thread, table walked at run time
+                              (n_dyn + n_reactions <= 32);
+                          1 = agent-per-wavefront: one 64-lane wave per agent,
+                              wave-reduced error norm, wave-uniform step
+                              control (n_dyn + n_reactions <= 512);
                           2 = agent-per-thread, network-specialised
                               (vk_table_specialize)                          */
 } vk_ode_opts;

@@ -17,6 +17,10 @@ struct vk_dev_table {
     int32_t o_rl_reaction, o_rl_enzyme, o_rl_kcat, o_rl_num_ptr, o_rl_den_ptr;
     int32_t o_set_ptr, o_mem_species, o_mem_param, o_upd_ptr, o_upd_rxn, o_ex_ptr, o_ex_rxn;
     int32_t o_upd_coeff, o_ex_coeff;
+    // reaction -> rate laws CSR (rate laws of reaction r in evaluation order),
+    // derived from rl_reaction at vk_table_create; the wavefront kernel sums
+    // flux[r] = 0 + v_l0 + v_l1 ... in the same order as the lane kernels
+    int32_t o_rx_ptr, o_rx_rl;
 };
 
 struct vk_table {

@@ -109,6 +109,14 @@ extern "C" int vk_table_create(const vk_table_desc *d, vk_table **out) {
     dbl.insert(dbl.end(), d->upd_coeff, d->upd_coeff + d->n_upd);
     dbl.insert(dbl.end(), d->ex_coeff, d->ex_coeff + d->n_exch);
     std::vector<int32_t> ints;
+    // reaction -> rate-law CSR (stable: evaluation order within a reaction)
+    std::vector<int32_t> rx_ptr(d->n_reactions + 1, 0), rx_rl(L);
+    for (int l = 0; l < L; ++l) rx_ptr[d->rl_reaction[l] + 1]++;
+    for (int r = 0; r < d->n_reactions; ++r) rx_ptr[r + 1] += rx_ptr[r];
+    {
+        std::vector<int32_t> fill(rx_ptr.begin(), rx_ptr.end() - 1);
+        for (int l = 0; l < L; ++l) rx_rl[fill[d->rl_reaction[l]]++] = l;
+    }
     struct Seg { const int32_t *src; size_t n; size_t off; };
     Seg segs[] = {
         {d->rl_reaction, (size_t)L, 0}, {d->rl_enzyme, (size_t)L, 0}, {d->rl_kcat, (size_t)L, 0},
@@ -117,6 +125,7 @@ extern "C" int vk_table_create(const vk_table_desc *d, vk_table **out) {
         {d->mem_param, (size_t)d->n_members, 0}, {d->upd_ptr, (size_t)d->n_dyn + 1, 0},
         {d->upd_rxn, (size_t)d->n_upd, 0}, {d->ex_ptr, (size_t)d->n_ext + 1, 0},
         {d->ex_rxn, (size_t)d->n_exch, 0},
+        {rx_ptr.data(), rx_ptr.size(), 0}, {rx_rl.data(), rx_rl.size(), 0},
     };
     for (auto &s : segs) {
         s.off = ints.size();
@@ -153,6 +162,7 @@ extern "C" int vk_table_create(const vk_table_desc *d, vk_table **out) {
     v.o_mem_species = (int32_t)segs[6].off; v.o_mem_param = (int32_t)segs[7].off;
     v.o_upd_ptr = (int32_t)segs[8].off; v.o_upd_rxn = (int32_t)segs[9].off;
     v.o_ex_ptr = (int32_t)segs[10].off; v.o_ex_rxn = (int32_t)segs[11].off;
+    v.o_rx_ptr = (int32_t)segs[12].off; v.o_rx_rl = (int32_t)segs[13].off;
     *out = t;
     return VK_OK;
 }
@@ -600,6 +610,273 @@ __global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t
     if (nsteps_out) nsteps_out[a] = ns;
 }
 
+// ---------------------------------------------------------------------------
+// Dormand-Prince 5(4), agent per WAVEFRONT (networks too large for a lane)
+// ---------------------------------------------------------------------------
+//
+// One 64-lane wavefront integrates one agent (one wave per workgroup, so
+// __syncthreads() is a wave barrier).  Component i of y = [dyn species |
+// flux integrals] lives in lane i % 64, slot i / 64 (NSLOT slots per lane).
+// Each RHS: lanes publish their species to the agent's LDS tile, lane l
+// evaluates rate laws l, l+64, ... (same arithmetic as rate_law_tile), lane r
+// sums reaction r's rate laws in evaluation order, lanes form dy for their
+// components.  The RMS error norm is a wavefront sum (DPP/shuffle butterfly),
+// so step acceptance, h and t are wave-uniform: no divergence at all.
+// Results agree with the lane kernels to rounding (only the order of the
+// norm's sum differs).
+
+constexpr int DW = 64;
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// rate law l from the agent's LDS tile (cl: species, pl: kcat or 1/Km);
+// table indices are lane-divergent here, so they are plain (vector) loads
+__device__ __forceinline__ double rate_law_wave(const vk_dev_table &t, int l, const double *cl, const double *pl) {
+    const int32_t *ib = t.ib;
+    double num = 0.0;
+    const int ns0 = ib[t.o_rl_num_ptr + l], ns1 = ib[t.o_rl_num_ptr + l + 1];
+    const double kcat = pl[ib[t.o_rl_kcat + l]];
+    for (int s = ns0; s < ns1; ++s) {
+        double term = kcat;
+        const int m0 = ib[t.o_set_ptr + s], m1 = ib[t.o_set_ptr + s + 1];
+        for (int m = m0; m < m1; ++m) term *= cl[ib[t.o_mem_species + m]] * pl[ib[t.o_mem_param + m]];
+        num += term;
+    }
+    num *= cl[ib[t.o_rl_enzyme + l]];
+    double den = 1.0;
+    const int ds0 = ib[t.o_rl_den_ptr + l], ds1 = ib[t.o_rl_den_ptr + l + 1];
+    for (int s = ds0; s < ds1; ++s) {
+        double term = 1.0;
+        const int m0 = ib[t.o_set_ptr + s], m1 = ib[t.o_set_ptr + s + 1];
+        for (int m = m0; m < m1; ++m) term *= fma(cl[ib[t.o_mem_species + m]], pl[ib[t.o_mem_param + m]], 1.0);
+        den += term - 1.0;
+    }
+    return num / den;
+}
+
+template <int NSLOT>
+__device__ __forceinline__ void rhs_wave(const vk_dev_table &t, const double (&y)[NSLOT], double (&dy)[NSLOT],
+                                         double *cl, double *fl, const double *pl, double *rl, int lane) {
+    const int nd = t.n_dyn, nr = t.n_reactions, nl = t.n_rate_laws;
+    const int32_t *ib = t.ib;
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+        const int i = lane + DW * k;
+        if (i < nd) cl[i] = y[k];
+    }
+    __syncthreads();
+    for (int l = lane; l < nl; l += DW) rl[l] = rate_law_wave(t, l, cl, pl);
+    __syncthreads();
+    for (int r = lane; r < nr; r += DW) {
+        double f = 0.0;
+        for (int k = ib[t.o_rx_ptr + r]; k < ib[t.o_rx_ptr + r + 1]; ++k) f += rl[ib[t.o_rx_rl + k]];
+        fl[r] = f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+        const int i = lane + DW * k;
+        double d = 0.0;
+        if (i < nd) {
+            for (int j = ib[t.o_upd_ptr + i]; j < ib[t.o_upd_ptr + i + 1]; ++j)
+                d = fma(t.db[t.o_upd_coeff + j], fl[ib[t.o_upd_rxn + j]], d);
+        } else if (i < nd + nr) {
+            d = fl[i - nd];
+        }
+        dy[k] = d;
+    }
+    __syncthreads();   // the next RHS overwrites cl / fl
+}
+
+template <int NSLOT>
+__device__ __forceinline__ double wave_rms(const double (&v)[NSLOT], const double (&sc)[NSLOT], int lane, int ny) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+        if (lane + DW * k < ny) {
+            const double q = v[k] / sc[k];
+            s = fma(q, q, s);
+        }
+    }
+    return sqrt(wave_sum(s) / ny);
+}
+
+template <int NSLOT>
+__global__ __launch_bounds__(DW) void k_dopri5_wave(vk_dev_table t, int64_t n, int64_t ld, double dt, double rtol,
+                                                    double atol, int max_steps, const double *__restrict__ params,
+                                                    double *__restrict__ conc, const double *__restrict__ m2c,
+                                                    double *__restrict__ delta, double *__restrict__ h_state,
+                                                    double *__restrict__ flux, int64_t *__restrict__ counts,
+                                                    int32_t *__restrict__ status, int32_t *__restrict__ nsteps_out) {
+    extern __shared__ double lds[];
+    const int lane = threadIdx.x;
+    const int64_t a = blockIdx.x;
+    if (a >= n) return;
+    const int ns_ = t.n_species, nr = t.n_reactions, np_ = t.n_params, nd = t.n_dyn;
+    const int ny = nd + nr;
+    double *cl = lds;                 // [n_species]
+    double *fl = cl + ns_;            // [n_reactions]
+    double *pl = fl + nr;             // [n_params]  kcat or 1/Km
+    double *rl = pl + np_;            // [n_rate_laws]
+    const int32_t *ib = t.ib;
+
+    for (int s = lane; s < ns_; s += DW) cl[s] = conc[(int64_t)s * ld + a];
+    for (int p = lane; p < np_; p += DW) pl[p] = params[(int64_t)p * ld + a];
+    __syncthreads();
+    const int n_mem = ib[t.o_set_ptr + ib[t.o_rl_den_ptr + t.n_rate_laws]];
+    for (int m = lane; m < n_mem; m += DW) {
+        const int p = ib[t.o_mem_param + m];
+        const double km = params[(int64_t)p * ld + a];
+        pl[p] = (km != 0.0) ? 1.0 / km : 0.0;
+    }
+    __syncthreads();
+
+    double y[NSLOT], k1[NSLOT], k2[NSLOT], k3[NSLOT], k4[NSLOT], k5[NSLOT], k6[NSLOT], k7[NSLOT], yt[NSLOT];
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+        const int i = lane + DW * k;
+        y[k] = (i < nd) ? cl[i] : 0.0;
+    }
+    rhs_wave<NSLOT>(t, y, k1, cl, fl, pl, rl, lane);
+    int32_t st = 0;
+    double h = h_state ? h_state[a] : 0.0;
+    if (!(h > 0.0)) {   // scipy select_initial_step (order 4)
+        double sc[NSLOT];
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) sc[k] = fma(fabs(y[k]), rtol, atol);
+        const double d0 = wave_rms<NSLOT>(y, sc, lane, ny), d1 = wave_rms<NSLOT>(k1, sc, lane, ny);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = fmin(h0, dt);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) yt[k] = fma(h0, k1[k], y[k]);
+        rhs_wave<NSLOT>(t, yt, k2, cl, fl, pl, rl, lane);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) k2[k] = k2[k] - k1[k];
+        const double d2 = wave_rms<NSLOT>(k2, sc, lane, ny) / h0;
+        const double h1 = (d1 <= 1e-15 && d2 <= 1e-15) ? fmax(1e-6, h0 * 1e-3) : pow(0.01 / fmax(d1, d2), 0.2);
+        h = fmin(fmin(100.0 * h0, h1), dt);
+    }
+
+    double tt = 0.0, h_keep = h;
+    int nsteps = 0;
+    bool rejected = false;
+    while (tt < dt) {   // every quantity in the loop control is wave-uniform
+        if (nsteps >= max_steps) { st |= VK_AGENT_MAX_STEPS; break; }
+        if (h < 1e-14 * dt) { st |= VK_AGENT_H_UNDERFLOW; break; }
+        double hs = h;
+        bool last = false;
+        if (tt + hs >= dt) { hs = dt - tt; last = true; }
+        ++nsteps;
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) yt[k] = fma(hs, dp::a21 * k1[k], y[k]);
+        rhs_wave<NSLOT>(t, yt, k2, cl, fl, pl, rl, lane);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) yt[k] = fma(hs, fma(dp::a32, k2[k], dp::a31 * k1[k]), y[k]);
+        rhs_wave<NSLOT>(t, yt, k3, cl, fl, pl, rl, lane);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k)
+            yt[k] = fma(hs, fma(dp::a43, k3[k], fma(dp::a42, k2[k], dp::a41 * k1[k])), y[k]);
+        rhs_wave<NSLOT>(t, yt, k4, cl, fl, pl, rl, lane);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k)
+            yt[k] = fma(hs, fma(dp::a54, k4[k], fma(dp::a53, k3[k], fma(dp::a52, k2[k], dp::a51 * k1[k]))), y[k]);
+        rhs_wave<NSLOT>(t, yt, k5, cl, fl, pl, rl, lane);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k)
+            yt[k] = fma(hs, fma(dp::a65, k5[k], fma(dp::a64, k4[k], fma(dp::a63, k3[k],
+                        fma(dp::a62, k2[k], dp::a61 * k1[k])))), y[k]);
+        rhs_wave<NSLOT>(t, yt, k6, cl, fl, pl, rl, lane);
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k)
+            yt[k] = fma(hs, fma(dp::b6, k6[k], fma(dp::b5, k5[k], fma(dp::b4, k4[k],
+                        fma(dp::b3, k3[k], dp::b1 * k1[k])))), y[k]);
+        rhs_wave<NSLOT>(t, yt, k7, cl, fl, pl, rl, lane);
+        double e2 = 0.0;
+#pragma unroll
+        for (int k = 0; k < NSLOT; ++k) {
+            if (lane + DW * k < ny) {
+                const double err = hs * fma(dp::e7, k7[k], fma(dp::e6, k6[k], fma(dp::e5, k5[k],
+                                       fma(dp::e4, k4[k], fma(dp::e3, k3[k], dp::e1 * k1[k])))));
+                const double q = err / fma(fmax(fabs(y[k]), fabs(yt[k])), rtol, atol);
+                e2 = fma(q, q, e2);
+            }
+        }
+        const double en = sqrt(wave_sum(e2) / ny);
+        if (!isfinite(en)) { st |= VK_AGENT_NONFINITE; break; }
+        if (en < 1.0) {
+            double factor = (en == 0.0) ? dp::MAX_FACTOR : fmin(dp::MAX_FACTOR, dp::SAFETY * pow(en, -0.2));
+            if (rejected) factor = fmin(1.0, factor);
+            tt = last ? dt : tt + hs;
+#pragma unroll
+            for (int k = 0; k < NSLOT; ++k) { y[k] = yt[k]; k1[k] = k7[k]; }
+            h_keep = last ? fmax(h, hs * factor) : hs * factor;
+            h = hs * factor;
+            rejected = false;
+        } else {
+            h = hs * fmax(dp::MIN_FACTOR, dp::SAFETY * pow(en, -0.2));
+            rejected = true;
+        }
+    }
+
+    // write back: species, mean fluxes; integrals -> LDS for the exchange counts
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < NSLOT; ++k) {
+        const int i = lane + DW * k;
+        if (i < nd) {
+            bad |= !isfinite(y[k]);
+            const int64_t idx = (int64_t)i * ld + a;
+            if (delta)
+                delta[idx] = y[k] - conc[idx];
+            else
+                conc[idx] = y[k];
+        } else if (i < ny) {
+            fl[i - nd] = y[k];
+            flux[(int64_t)(i - nd) * ld + a] = y[k] / dt;
+        }
+    }
+    __syncthreads();
+    if (__any(bad)) st |= VK_AGENT_NONFINITE;
+    const double mc = m2c[a];
+    int32_t cst = 0;
+    for (int e = lane; e < t.n_ext; e += DW) {
+        int64_t c = 0;
+        for (int j = ib[t.o_ex_ptr + e]; j < ib[t.o_ex_ptr + e + 1]; ++j)
+            c += trunc_count((t.db[t.o_ex_coeff + j] * fl[ib[t.o_ex_rxn + j]]) * mc, cst);
+        counts[(int64_t)e * ld + a] = c;
+    }
+    if (__any(cst != 0)) st |= VK_AGENT_NONFINITE;
+    if (lane == 0) {
+        if (h_state) h_state[a] = h_keep;
+        if (status) status[a] = st;
+        if (nsteps_out) nsteps_out[a] = nsteps;
+    }
+}
+
+template <int NSLOT>
+static int launch_dopri5_wave(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,
+                              const double *params, double *conc, const double *m2c, double *delta,
+                              double *h_state, double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
+                              hipStream_t stream) {
+    const vk_dev_table &d = t->dev;
+    const size_t lds = (size_t)(d.n_species + d.n_reactions + d.n_params + d.n_rate_laws) * sizeof(double);
+    if (lds > 64 * 1024) {
+        vk::set_error("vk_step_dopri5: network needs %zu B of LDS per agent (> 64 KiB)", lds);
+        return VK_ERR_LIMIT;
+    }
+    if (n > 0x7fffffff) {
+        vk::set_error("vk_step_dopri5: agent-per-wavefront grid limited to 2^31-1 agents");
+        return VK_ERR_LIMIT;
+    }
+    hipLaunchKernelGGL(k_dopri5_wave<NSLOT>, dim3((unsigned)n), dim3(DW), lds, stream, d, n, ld, dt, o->rtol,
+                       o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux, counts, status, nsteps);
+    return vk::launch_check("k_dopri5_wave");
+}
+
 template <int NY>
 static int launch_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,
                          const double *params, double *conc, const double *m2c, double *delta, double *h_state,
@@ -651,12 +928,22 @@ extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double d
                                                    args, nullptr),
                              "hipModuleLaunchKernel(vk_dopri5_spec)");
     }
+    const int ny = t->dev.n_dyn + t->dev.n_reactions;
+    hipStream_t s = (hipStream_t)stream;
+    if (o->variant == 1) {  // agent per wavefront
+#define VK_DW(NS) return launch_dopri5_wave<NS>(t, n, ld, dt, o, params, conc, m2c, delta, h_state, flux, counts, status, nsteps, s)
+        if (ny <= 64) VK_DW(1);
+        if (ny <= 128) VK_DW(2);
+        if (ny <= 256) VK_DW(4);
+        if (ny <= 512) VK_DW(8);
+#undef VK_DW
+        vk::set_error("vk_step_dopri5: %d integrated components > 512 (agent-per-wavefront limit)", ny);
+        return VK_ERR_LIMIT;
+    }
     if (o->variant != 0) {
         vk::set_error("vk_step_dopri5: variant %d not available", o->variant);
         return VK_ERR_ARG;
     }
-    const int ny = t->dev.n_dyn + t->dev.n_reactions;
-    hipStream_t s = (hipStream_t)stream;
 #define VK_DP(NYC) return launch_dopri5<NYC>(t, n, ld, dt, o, params, conc, m2c, delta, h_state, flux, counts, status, nsteps, s)
     switch (ny) {
         case 1: VK_DP(1); case 2: VK_DP(2); case 3: VK_DP(3); case 4: VK_DP(4);

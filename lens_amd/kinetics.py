@@ -48,11 +48,20 @@ class KineticsEngine:
         Afterwards :meth:`dopri5` defaults to variant 2 (straight-line rate
         laws, everything in VGPRs) instead of the generic table walk."""
         from lens_amd.codegen import dopri5_source
+        if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:
+            return self   # too large for one lane: the agent-per-wavefront kernel serves it
         with torch.cuda.device(self.device):
             native.check(native._lib.vk_table_specialize(self.dev.handle, dopri5_source(self.table).encode()),
                          'vk_table_specialize')
         self.specialized = True
         return self
+
+    LANE_LIMIT = 32   # integrated components an agent-per-lane kernel holds in VGPRs
+
+    def default_variant(self) -> int:
+        if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:
+            return 1
+        return 2 if self.specialized else 0
 
     # -- allocation helpers -------------------------------------------------
     def empty_like_agents(self, rows, ld, dtype=F64):
@@ -109,12 +118,13 @@ class KineticsEngine:
                variant=None, delta=None):
         """Adaptive DP5(4) over [0, dt] in place on ``conc``.
 
-        ``variant``: 0 = generic table walk, 2 = network-specialised (default
-        once :meth:`specialize` ran).  Returns (flux = mean flux over dt,
-        counts, status, nsteps)."""
+        ``variant``: 0 = agent per lane, generic table walk; 1 = agent per
+        wavefront (default when n_dyn + n_reactions > 32); 2 = agent per lane,
+        network-specialised (default once :meth:`specialize` ran).  Returns
+        (flux = mean flux over dt, counts, status, nsteps)."""
         t = self.table
         if variant is None:
-            variant = 2 if self.specialized else 0
+            variant = self.default_variant()
         n = conc.shape[1] if n_agents is None else n_agents
         ld = self._check_state(params, conc, n)
         _need(mmol_to_counts, 'mmol_to_counts', None, ld, F64, self.device)

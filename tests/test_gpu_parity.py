@@ -132,8 +132,9 @@ def _params_dict(t, cfg, pvec):
     return kp
 
 
+@pytest.mark.parametrize('variant', [0, 1])
 @pytest.mark.parametrize('name', ['glc_lct', 'glc_ac', 'glc_lct_transport'])
-def test_dopri5_matches_odeint(dev, name):
+def test_dopri5_matches_odeint(dev, name, variant):
     """North-star bar: end states within 1e-6 relative of scipy odeint (LSODA).
 
     Tolerance: |gpu - odeint| <= 1e-6*|odeint| + 1e-10.  The absolute floor is
@@ -150,7 +151,7 @@ def test_dopri5_matches_odeint(dev, name):
     c_dev = torch.from_numpy(conc.copy()).to(dev)
     h = torch.zeros(n, dtype=torch.float64, device=dev)
     flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
-                                              torch.from_numpy(m2c).to(dev), h_state=h)
+                                              torch.from_numpy(m2c).to(dev), h_state=h, variant=variant)
     assert not status.cpu().numpy().any()
     got = c_dev.cpu().numpy()
     fl = flux.cpu().numpy()
@@ -203,12 +204,91 @@ def test_dopri5_status_and_limits(dev):
     eb = _engine(tb, dev)
     pb = torch.from_numpy(np.repeat(tb.param_defaults[:, None], 8, axis=1)).to(dev)
     cb = torch.ones((tb.n_species, 8), dtype=torch.float64, device=dev)
-    if tb.n_dyn + tb.n_reactions > 32:
-        with pytest.raises(NativeError):
-            eb.dopri5(1.0, pb, cb, torch.ones(8, dtype=torch.float64, device=dev))
+    assert tb.n_dyn + tb.n_reactions > 32
+    with pytest.raises(NativeError):
+        eb.dopri5(1.0, pb, cb, torch.ones(8, dtype=torch.float64, device=dev), variant=0)
+    with pytest.raises(NativeError):
+        eb.dopri5(1.0, pb, cb, torch.ones(8, dtype=torch.float64, device=dev), variant=7)
+    assert eb.default_variant() == 1
     with pytest.raises(ValueError):
         eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev[:, :10].contiguous(),
                    torch.ones(64, dtype=torch.float64, device=dev))
+
+
+def _big_network(ns=50, nr=40, ne=10, n=160, seed=20261015):
+    cfg = configs.synthetic_network(n_species=ns, n_reactions=nr, n_enzymes=ne, seed=seed)
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=seed + 1, sigma=0.2)
+    return cfg, t, params, conc
+
+
+@pytest.mark.parametrize('shape', [(50, 40, 10), (30, 20, 6), (120, 90, 12)])
+def test_dopri5_wave_vs_c_oracle(dev, shape):
+    """Agent-per-wavefront DP45 (C5-size networks) == the C oracle's DP45 to
+    rounding: same RHS arithmetic, same step control; only the order of the
+    error norm's sum differs (a wave reduction)."""
+    cfg, t, params, conc = _big_network(*shape)
+    n = conc.shape[1]
+    assert t.n_dyn + t.n_reactions > 32
+    m2c = np.full(n, mmol_to_counts())
+    eng = _engine(t, dev)
+    assert eng.default_variant() == 1
+    c_dev = torch.from_numpy(conc.copy()).to(dev)
+    h = torch.zeros(n, dtype=torch.float64, device=dev)
+    flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
+                                              torch.from_numpy(m2c).to(dev), h_state=h)
+    assert not status.cpu().numpy().any()
+    c_ref = conc.copy()
+    hr = np.zeros(n)
+    f_ref, k_ref, s_ref, n_ref = cpu.step_dopri5(cpu.Desc(t), 1.0, params, c_ref, m2c, h_state=hr)
+    got = c_dev.cpu().numpy()
+    scale = np.abs(c_ref[:t.n_dyn]) + 1e-9 * np.abs(c_ref[:t.n_dyn]).max(axis=0)
+    assert (np.abs(got[:t.n_dyn] - c_ref[:t.n_dyn]) / scale).max() < 1e-9
+    assert np.mean(nsteps.cpu().numpy() == n_ref) > 0.95
+    fl = flux.cpu().numpy()
+    fscale = np.abs(f_ref) + 1e-9 * np.abs(f_ref).max(axis=0)
+    assert (np.abs(fl - f_ref) / fscale).max() < 1e-9
+    # exchange counts come from the flux integrals: equal up to a one-count
+    # truncation flip where the integral sits on an integer boundary
+    assert np.abs(counts.cpu().numpy() - k_ref).max() <= 1
+
+
+def test_dopri5_wave_matches_odeint(dev):
+    """North-star bar on a 50-species network: within 1e-6 relative of odeint."""
+    cfg, t, params, conc = _big_network(n=24)
+    n = conc.shape[1]
+    m2c = np.full(n, mmol_to_counts())
+    eng = _engine(t, dev)
+    c_dev = torch.from_numpy(conc.copy()).to(dev)
+    flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
+                                              torch.from_numpy(m2c).to(dev), rtol=1e-10, atol=1e-14)
+    assert not status.cpu().numpy().any()
+    got = c_dev.cpu().numpy()
+    for a in range(0, n, 5):
+        ode = OracleODE(cfg['reactions'], _params_dict(t, cfg, params[:, a]))
+        new, mean_flux, cnt = ode.step({k: conc[s, a] for s, k in enumerate(t.species)}, 1.0, m2c[a])
+        for s_ in range(t.n_dyn):
+            ref = new[t.species[s_]]
+            assert abs(got[s_, a] - ref) <= 1e-6 * abs(ref) + 1e-10, (a, t.species[s_], got[s_, a], ref)
+
+
+def test_dopri5_wave_equals_lane_variant_small_network(dev):
+    """Both kernels on glc_lct: same trajectory to rounding."""
+    cfg = configs.glc_lct_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    n = 2000
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=3)
+    m2c = torch.full((n,), mmol_to_counts(), dtype=torch.float64, device=dev)
+    eng = _engine(t, dev)
+    out = []
+    for variant in (0, 1):
+        c_dev = torch.from_numpy(conc.copy()).to(dev)
+        flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev, m2c,
+                                                  variant=variant)
+        out.append((c_dev.cpu().numpy(), nsteps.cpu().numpy()))
+    rel = np.abs(out[0][0] - out[1][0]) / (np.abs(out[0][0]) + 1e-300)
+    assert rel[:t.n_dyn].max() < 1e-10
+    assert np.mean(out[0][1] == out[1][1]) > 0.99
 
 
 @pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (1, 3), (1, 7), (1, 11), (1, 15)])
