@@ -220,6 +220,117 @@ int vk_bin_sites(const double *loc, int64_t n_agents, int64_t ld, int32_t nx, in
                  double bound_x, double bound_y, int32_t row_offset, int32_t *bin_lin,
                  int32_t *ix_out, vk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Cell growth, derivers and division
+ *
+ *   vk_cell_step
+ *       replaces, per agent and step, GrowthProtein.next_update
+ *       (vivarium/processes/growth_protein.py:88-107) or Growth.next_update
+ *       (growth.py:101-107) + DivisionVolume.next_update (division_volume.py:
+ *       39-45) -- all from the step-start state -- followed by the derivers
+ *       TreeMass (tree_mass.py:10-18) and DeriveGlobals.next_update
+ *       (derive_globals.py:131-152) on the updated state.  Writes divide[a].
+ *   vk_divide_plan + vk_divide_gather / vk_divide_lineage / vk_divide_locations
+ *       replace MetaDivision.next_update (meta_division.py:60-88) and the
+ *       `_divide` branch of Store.apply_update (core/experiment.py:664-697)
+ *       with its dividers (core/registry.py:197-280): the new agent order is
+ *       the survivors in order, then daughters id+'0', id+'1' of each mother
+ *       in mother order; mothers are removed.
+ * ------------------------------------------------------------------------- */
+
+/* Rows of the per-agent cell array cell[VK_CELL_ROWS][ld] ("global" port). */
+enum vk_cell_row {
+    VK_CELL_MASS = 0,         /* fg                                  split */
+    VK_CELL_VOLUME = 1,       /* fL                                  split */
+    VK_CELL_LENGTH = 2,       /* um                                  split */
+    VK_CELL_SURFACE_AREA = 3, /* um^2                                split */
+    VK_CELL_PROTEIN = 4,      /* counts (float, as the reference)    split */
+    VK_CELL_ANGLE = 5,        /* rad (orientation for daughter locations) set */
+    VK_CELL_ROWS = 6
+};
+
+enum vk_growth_model {
+    VK_GROWTH_PROTEIN = 0,  /* GrowthProtein + TreeMass; divide when protein >= divide_protein */
+    VK_GROWTH_MASS = 1      /* Growth (mass*factor); DivisionVolume: divide when volume >= division_volume */
+};
+
+enum vk_rng {
+    VK_RNG_STREAM = 0,      /* uniforms u[a] supplied by the caller in agent order (e.g. numpy's
+                               MT19937 stream, which replays the reference exactly)            */
+    VK_RNG_PHILOX = 1       /* Philox4x32-10 counter = (step, root, path lo, path hi),
+                               key = (seed lo + depth, seed hi): order-independent               */
+};
+
+typedef struct vk_cell_params {
+    int32_t model;            /* vk_growth_model                                     */
+    int32_t rng;              /* vk_rng (VK_GROWTH_PROTEIN only)                     */
+    double factor;            /* exp(growth_rate * dt), evaluated by the host        */
+    double divide_protein;    /* GrowthProtein: 2 * initial protein                  */
+    double division_volume;   /* DivisionVolume threshold (fL)                       */
+    double protein_mw;        /* g/mol                                               */
+    double avogadro;          /* 1/mol                                               */
+    double fg_per_g;          /* g -> fg factor as the reference's units evaluate it */
+    double density;           /* g/L                                                 */
+    double volume_to_fl;      /* fg*L/g -> fL factor as the reference evaluates it   */
+    /* capsule constants of the (colony-wide) width w, r = w/2, evaluated by the host
+       exactly as derive_globals.py:20-50 writes them                                 */
+    double cap_volume;        /* (4/3)*PI*r**3                                       */
+    double cap_area;          /* PI*r**2                                             */
+    double two_r;             /* 2*r                                                 */
+    double width;             /* w                                                   */
+    double sa_const;          /* 3*PI*r**2                                           */
+    double sa_lin;            /* 2*PI*r                                              */
+    uint64_t seed;            /* VK_RNG_PHILOX                                       */
+    uint64_t step;            /* VK_RNG_PHILOX counter word                          */
+} vk_cell_params;
+
+/* Lineage (phylogeny id) of agent a: root[a] indexes the caller's root ids,
+ * the id string is root id + the depth[a] low bits of path[a], MSB first.   */
+
+/* Growth process + derivers for agents [0, n).  u: [ld] uniforms (VK_RNG_STREAM)
+ * or NULL; root/depth/path: lineage (VK_RNG_PHILOX) or NULL.  cell rows and
+ * mmol_to_counts are updated in place; divide[a] = 0/1.                     */
+int vk_cell_step(const vk_cell_params *p, int64_t n_agents, int64_t ld, double *cell,
+                 double *mmol_to_counts, const double *u, const int32_t *root,
+                 const int32_t *depth, const uint64_t *path, int32_t *divide,
+                 vk_stream_t stream);
+
+/* Division plan: src_index[j] = source agent of new slot j, kind[j] = -1 for a
+ * survivor, 0 / 1 for daughter 0 / 1 (j < n_agents + n_divide).  n_out: one
+ * device int64 (new agent count).  scratch: >= vk_divide_scratch_bytes(n).
+ * The new count must fit the destination capacity the caller then uses.    */
+int64_t vk_divide_scratch_bytes(int64_t n_agents);
+int vk_divide_plan(const int32_t *divide, int64_t n_agents, int32_t *src_index, int32_t *kind,
+                   int64_t *n_out, void *scratch, vk_stream_t stream);
+
+enum vk_divider {
+    VK_DIVIDE_SET = 0,     /* both daughters copy the mother's value (no divider)  */
+    VK_DIVIDE_SPLIT = 1,   /* float64 halves (registry.py divide_split, floats)     */
+    VK_DIVIDE_ZERO = 2     /* daughters get 0 (divide flags: meta_division.py:21)   */
+};
+
+/* dst[r*ld_dst + j] = divider(src[r*ld_src + src_index[j]]) for rows [0, rows),
+ * slots [0, n_out); elem_bytes 4 or 8 (SPLIT: 8 = float64 only).            */
+int vk_divide_gather(int64_t n_out, const int32_t *src_index, const int32_t *kind,
+                     const void *src, int64_t ld_src, void *dst, int64_t ld_dst, int32_t rows,
+                     int32_t elem_bytes, int32_t divider, vk_stream_t stream);
+
+/* Lineage divider (daughter_phylogeny_id, meta_division.py:15-18): daughter k
+ * of (root, depth, path) is (root, depth+1, path*2+k).  Sets *overflow (device
+ * int32, nullable) when a lineage would exceed 64 generations.              */
+int vk_divide_lineage(int64_t n_out, const int32_t *src_index, const int32_t *kind,
+                      const int32_t *root_src, const int32_t *depth_src, const uint64_t *path_src,
+                      int32_t *root_dst, int32_t *depth_dst, uint64_t *path_dst,
+                      int32_t *overflow, vk_stream_t stream);
+
+/* daughter_locations (multibody_physics.py:77-87): daughter k of a mother at
+ * (x, y) with length L and angle t sits at (x + L*q*cos t, y + L*q*sin t),
+ * q = -0.25 / +0.25.  loc_* are [2][ld] (x row, y row); the mother's length
+ * and angle are read from the gathered cell rows (length already split).    */
+int vk_divide_locations(int64_t n_out, const int32_t *src_index, const int32_t *kind,
+                        const double *loc_src, int64_t ld_src, double *loc_dst, int64_t ld_dst,
+                        const double *cell_dst, vk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

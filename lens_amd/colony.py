@@ -17,16 +17,24 @@ a :class:`~lens_amd.lattice.Lattice` (configs 3-4; DiffusionField + agents)
     -> diffusion substeps -> exchange scatter in agent order.
 
 Step order and quirks follow SURVEY.md Appendix A.5.
+
+With a :class:`~lens_amd.cells.CellModel` the step continues like the
+reference's deriver pass: the growth process (from the step-start state),
+then TreeMass / DeriveGlobals (``mmol_to_counts`` for the next step's
+exchange), then division: survivors keep their order, daughters are appended
+in mother order, every per-agent array is gathered once with its divider.
 """
 
 from __future__ import annotations
 
+import ctypes
 from typing import Optional
 
 import numpy as np
 import torch
 
 from lens_amd import native
+from lens_amd.cells import CellModel, lineage_ids
 from lens_amd.configs import initial_conc
 from lens_amd.kinetics import KineticsEngine
 from lens_amd.lattice import Lattice, occupancy, N_A_LEGACY
@@ -43,7 +51,8 @@ class Colony:
                  integrator: str = 'dopri5', rtol: float = 1e-8, atol: float = 1e-12,
                  max_steps: int = 100000, environment='held', env_volume_L: float = 1e-14,
                  avogadro: float = N_A_LEGACY, exchange: str = 'sorted', mass_fg: float = 1339.0,
-                 table: Optional[RateLawTable] = None, specialize: bool = False):
+                 table: Optional[RateLawTable] = None, specialize: bool = False,
+                 cells: Optional[CellModel] = None, agent_ids=None):
         if integrator not in ('euler', 'dopri5'):
             raise ValueError('integrator must be euler or dopri5')
         if exchange not in ('sorted', 'atomic'):
@@ -73,7 +82,24 @@ class Colony:
         self.nsteps = z(ld, dtype=torch.int32)
         self.h_state = z(ld)
         self.time = 0.0
+        self.step_index = 0
         self.lattice: Optional[Lattice] = None
+        self.location = None
+        self.env_fields = None
+        self.cells = cells
+        if cells is not None:
+            rows, m2c = cells.initial_rows(ld)
+            self.cell = torch.from_numpy(rows).to(dev).contiguous()
+            self.m2c.copy_(torch.from_numpy(m2c))
+            self.divide = z(ld, dtype=torch.int32)
+            self.roots = [str(i) for i in range(self.n)] if agent_ids is None else [str(x) for x in agent_ids]
+            if len(self.roots) != self.n:
+                raise ValueError('agent_ids must name every agent')
+            self.lin_root = torch.arange(ld, dtype=torch.int32, device=dev)
+            self.lin_depth = z(ld, dtype=torch.int32)
+            self.lin_path = z(ld, dtype=torch.int64)
+            self._n_out = torch.zeros(1, dtype=torch.int64, device=dev)
+            self._overflow = torch.zeros(1, dtype=torch.int32, device=dev)
         self.environment = environment
         if isinstance(environment, Lattice):
             self.lattice = environment
@@ -194,7 +220,97 @@ class Colony:
                     native.ptr(self.map_exch_field), int(self.map_exch_count.numel()),
                     self.env_binvol_avogadro, native.stream_handle()), 'vk_exchange_atomic')
             self._env_to_external()
+        if self.cells is not None:
+            self.grow_and_divide(dt)
         self.time += dt
+        self.step_index += 1
+
+    # -- growth, derivers, division (a10-a13) ------------------------------------
+    def grow_and_divide(self, dt: float):
+        """Growth process + TreeMass/DeriveGlobals, then division.  Returns the
+        number of mothers that divided."""
+        cm, n = self.cells, self.n
+        if n == 0:
+            return 0
+        p = cm.vk_params(dt, self.step_index)
+        u = None
+        if cm.model == 'growth_protein' and cm.rng == 'stream':
+            u = torch.from_numpy(cm.host_uniforms(n)).to(self.device)
+        native.check(native._lib.vk_cell_step(
+            ctypes.byref(p), n, self.ld, native.ptr(self.cell), native.ptr(self.m2c), native.ptr(u),
+            native.ptr(self.lin_root), native.ptr(self.lin_depth), native.ptr(self.lin_path),
+            native.ptr(self.divide), native.stream_handle()), 'vk_cell_step')
+        src = torch.empty(2 * n, dtype=torch.int32, device=self.device)
+        kind = torch.empty(2 * n, dtype=torch.int32, device=self.device)
+        scratch = torch.empty(int(native._lib.vk_divide_scratch_bytes(n)), dtype=torch.uint8, device=self.device)
+        native.check(native._lib.vk_divide_plan(
+            native.ptr(self.divide), n, native.ptr(src), native.ptr(kind), native.ptr(self._n_out),
+            native.ptr(scratch), native.stream_handle()), 'vk_divide_plan')
+        n_out = int(self._n_out.item())
+        if n_out == n:
+            return 0
+        self._apply_division(n_out, src, kind)
+        return n_out - n
+
+    def _apply_division(self, n_out, src, kind):
+        ld_src = self.ld
+        ld = max(self.ld, n_out)
+        if n_out > self.ld:
+            ld = max(n_out, int(self.ld * 1.25) + 64)
+        dev, st = self.device, native.stream_handle()
+        S, SP, Z = native.VK_DIVIDE_SET, native.VK_DIVIDE_SPLIT, native.VK_DIVIDE_ZERO
+
+        def gather(t, divider=S, rows_slice=None):
+            rows = 1 if t.dim() == 1 else t.shape[0]
+            out = torch.empty((ld,) if t.dim() == 1 else (rows, ld), dtype=t.dtype, device=dev)
+            native.check(native._lib.vk_divide_gather(
+                n_out, native.ptr(src), native.ptr(kind), native.ptr(t), ld_src, native.ptr(out), ld, rows,
+                t.element_size(), divider, st), 'vk_divide_gather')
+            return out
+
+        for name in ('params', 'conc', 'm2c', 'flux', 'counts', 'status', 'nsteps', 'h_state'):
+            setattr(self, name, gather(getattr(self, name)))
+        if self.env_fields is not None:
+            self.env_fields = gather(self.env_fields)
+            self.env_bins = torch.arange(ld, dtype=torch.int32, device=dev)
+        cell = torch.empty((native.VK_CELL_ROWS, ld), dtype=torch.float64, device=dev)
+        n_split = native.VK_CELL_ANGLE      # rows [0, angle) split, angle copied
+        native.check(native._lib.vk_divide_gather(
+            n_out, native.ptr(src), native.ptr(kind), native.ptr(self.cell), ld_src, native.ptr(cell), ld,
+            n_split, 8, SP, st), 'vk_divide_gather(cell)')
+        native.check(native._lib.vk_divide_gather(
+            n_out, native.ptr(src), native.ptr(kind), self.cell.data_ptr() + n_split * ld_src * 8, ld_src,
+            cell.data_ptr() + n_split * ld * 8, ld, native.VK_CELL_ROWS - n_split, 8, S, st),
+            'vk_divide_gather(angle)')
+        self.divide = gather(self.divide, Z)
+        root = torch.empty(ld, dtype=torch.int32, device=dev)
+        depth = torch.empty(ld, dtype=torch.int32, device=dev)
+        path = torch.empty(ld, dtype=torch.int64, device=dev)
+        native.check(native._lib.vk_divide_lineage(
+            n_out, native.ptr(src), native.ptr(kind), native.ptr(self.lin_root), native.ptr(self.lin_depth),
+            native.ptr(self.lin_path), native.ptr(root), native.ptr(depth), native.ptr(path),
+            native.ptr(self._overflow), st), 'vk_divide_lineage')
+        if self.location is not None:
+            loc = torch.empty((2, ld), dtype=torch.float64, device=dev)
+            native.check(native._lib.vk_divide_locations(
+                n_out, native.ptr(src), native.ptr(kind), native.ptr(self.location), ld_src, native.ptr(loc), ld,
+                native.ptr(cell), st), 'vk_divide_locations')
+            self.location = loc
+        self.cell, self.lin_root, self.lin_depth, self.lin_path = cell, root, depth, path
+        self.n, self.ld = n_out, ld
+        if self.lattice is not None:
+            self.bin_lin = torch.zeros(ld, dtype=torch.int32, device=dev)
+            self.bin_ix = torch.zeros(ld, dtype=torch.int32, device=dev)
+            self.refresh_bins()
+        if int(self._overflow.item()):
+            raise OverflowError('a lineage exceeded 64 generations (phylogeny path bits)')
+
+    def agent_ids(self):
+        """Phylogeny ids of agents 0..n-1 (meta_division.py:15-18)."""
+        if self.cells is None:
+            return [str(a) for a in range(self.n)]
+        return lineage_ids(self.roots, self.lin_root[:self.n].cpu().numpy(),
+                           self.lin_depth[:self.n].cpu().numpy(), self.lin_path[:self.n].cpu().numpy())
 
     def check_status(self):
         st = self.status[:self.n]
@@ -215,4 +331,13 @@ class Colony:
             out.setdefault(port, {})[name] = c[s].copy()
         f = self.flux[:, :self.n].cpu().numpy()
         out['fluxes'] = {rid: f[r].copy() for r, rid in enumerate(self.table.reaction_ids)}
+        if self.cells is not None:
+            c = self.cell[:, :self.n].cpu().numpy()
+            out['global'] = {name: c[row].copy() for name, row in (
+                ('mass', native.VK_CELL_MASS), ('volume', native.VK_CELL_VOLUME),
+                ('length', native.VK_CELL_LENGTH), ('surface_area', native.VK_CELL_SURFACE_AREA),
+                ('angle', native.VK_CELL_ANGLE))}
+            out['global']['width'] = np.full(self.n, self.cells.width)
+            out['global']['mmol_to_counts'] = self.m2c[:self.n].cpu().numpy().copy()
+            out.setdefault('internal', {})['protein'] = c[native.VK_CELL_PROTEIN].copy()
         return out

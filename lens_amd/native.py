@@ -28,8 +28,15 @@ EXPORTS = (
     'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy', 'vk_table_specialize',
     'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_field_uniform',
     'vk_diffuse', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_gather', 'vk_exchange_sorted',
-    'vk_exchange_atomic', 'vk_bin_sites',
+    'vk_exchange_atomic', 'vk_bin_sites', 'vk_cell_step', 'vk_divide_scratch_bytes', 'vk_divide_plan',
+    'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations',
 )
+
+VK_CELL_MASS, VK_CELL_VOLUME, VK_CELL_LENGTH, VK_CELL_SURFACE_AREA, VK_CELL_PROTEIN, VK_CELL_ANGLE = range(6)
+VK_CELL_ROWS = 6
+VK_GROWTH_PROTEIN, VK_GROWTH_MASS = 0, 1
+VK_RNG_STREAM, VK_RNG_PHILOX = 0, 1
+VK_DIVIDE_SET, VK_DIVIDE_SPLIT, VK_DIVIDE_ZERO = 0, 1, 2
 
 
 class NativeError(RuntimeError):
@@ -60,6 +67,14 @@ class VkOdeOpts(ctypes.Structure):
                 ('max_steps', ctypes.c_int32), ('variant', ctypes.c_int32)]
 
 
+class VkCellParams(ctypes.Structure):
+    _fields_ = [('model', ctypes.c_int32), ('rng', ctypes.c_int32)] + [
+        (n, ctypes.c_double) for n in (
+            'factor', 'divide_protein', 'division_volume', 'protein_mw', 'avogadro', 'fg_per_g',
+            'density', 'volume_to_fl', 'cap_volume', 'cap_area', 'two_r', 'width', 'sa_const',
+            'sa_lin')] + [('seed', ctypes.c_uint64), ('step', ctypes.c_uint64)]
+
+
 _SIGS = {
     'vk_abi_version': ([], ctypes.c_int),
     'vk_last_error': ([], ctypes.c_char_p),
@@ -80,6 +95,13 @@ _SIGS = {
                            ctypes.c_int),
     'vk_exchange_atomic': ([_vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _i32, _f64, _vp], ctypes.c_int),
     'vk_bin_sites': ([_vp, _i64, _i64, _i32, _i32, _f64, _f64, _i32, _vp, _vp, _vp], ctypes.c_int),
+    'vk_cell_step': ([ctypes.POINTER(VkCellParams), _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+                     ctypes.c_int),
+    'vk_divide_scratch_bytes': ([_i64], ctypes.c_int64),
+    'vk_divide_plan': ([_vp, _i64, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
+    'vk_divide_gather': ([_i64, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp], ctypes.c_int),
+    'vk_divide_lineage': ([_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
+    'vk_divide_locations': ([_i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
 }
 
 _lib = None

@@ -206,5 +206,42 @@ def main():
     print('wrote', len(cases), 'flux cases')
 
 
+def colony_metrics_fixture():
+    """colony_metrics_subset.npz from vivarium/reference_data/colony_metrics.csv
+    (the reference's division / phylogeny golden): for each of the 30 agent ids
+    its number of emitted rows (lifetime; later-born agents' columns are padded
+    from row 0, vivarium/library/timeseries.py:53-69) and the mass, volume,
+    width, length, surface_area, protein values at every 10th row plus the
+    first and last three rows of its life."""
+    src = '/root/reference/vivarium/reference_data/colony_metrics.csv'
+    with open(src) as f:
+        rows = list(csv.reader(f))
+    header, body = rows[0], rows[1:]
+    cols = {tuple(h.split(',')[1:]): i for i, h in enumerate(header)}
+    ids = []
+    for h in header:
+        parts = h.split(',')
+        if parts[0] == 'agents' and parts[1] not in ids:
+            ids.append(parts[1])
+    variables = ('mass', 'volume', 'width', 'length', 'surface_area', 'protein')
+    out = {'ids': np.array(ids), 'variables': np.array(variables)}
+    for aid in ids:
+        series = []
+        for v in variables:
+            i = cols[(aid, 'internal' if v == 'protein' else 'boundary', v)]
+            series.append([float(r[i]) for r in body if r[i] != ''])
+        n = len(series[0])
+        keep = sorted(set(list(range(0, n, 10)) + [0, 1, 2, n - 3, n - 2, n - 1]))
+        out['n_' + aid] = np.array(n)
+        out['k_' + aid] = np.array(keep)
+        out['v_' + aid] = np.array([[series[j][k] for j in range(len(variables))] for k in keep])
+    np.savez_compressed(os.path.join(HERE, 'colony_metrics_subset.npz'), **out)
+    print('wrote colony_metrics_subset.npz:', len(ids), 'agents')
+
+
 if __name__ == '__main__':
-    main()
+    if '--colony-metrics' in sys.argv:
+        colony_metrics_fixture()
+    else:
+        main()
+        colony_metrics_fixture()

@@ -13,7 +13,7 @@ HEADER = os.path.join(REPO, 'include', 'vk_kinetics.h')
 
 def declared_symbols():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r'^\s*(?:int|const char \*)\s*(vk_\w+)\s*\(', text, re.M)))
+    return sorted(set(re.findall(r'^\s*(?:int|int64_t|const char \*)\s*(vk_\w+)\s*\(', text, re.M)))
 
 
 def test_header_declares_the_boundary():
