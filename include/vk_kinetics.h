@@ -331,6 +331,33 @@ int vk_divide_locations(int64_t n_out, const int32_t *src_index, const int32_t *
                         const double *loc_src, int64_t ld_src, double *loc_dst, int64_t ld_dst,
                         const double *cell_dst, vk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * Kremling 2007 sugar transport: the reference's only odeint
+ * call, Transport.next_update (vivarium/processes/Kremling2007_transport.py:
+ * 218-427).  DEFAULT_PARAMETERS (:19-70) in this field order; units as the
+ * reference (time in hours).
+ * ------------------------------------------------------------------------- */
+typedef struct vk_kremling_params {
+    double k1, k2, k3, K1, K2, K3, kd, m, n, x0, kg6p, Kg6p, kptsup, Kglc, Keiiap, klac, Km_lac,
+        Kieiia, kgly, kpyk, kpdh, kpts, km_pts, mw1, mw2, mw3, Y1_sim, Y2_sim, Y3_sim, K, kb, ksyn,
+        KI;
+} vk_kremling_params;
+
+/* state[15][ld]: mass, UHPT, LACZ, PTSG, G6P, PEP, PYR, XP, GLC[e], G6P[e],
+ * LCTS[e], then 4 scratch rows (flux integrals GLCpts, PPS, PYK, glc__D_e).
+ * Integrates over the reference's grid t_i = i*grid_h (hours), i <
+ * n_grid (np.arange(0, dt/3600, 0.01/3600): 100 points, last at 0.99 s),
+ * landing on every grid point.  Rows 0-7 := y(t_last); rows 8-10 (external)
+ * are left as they were; flux[4][ld] := mean over the grid points of the
+ * integrals; counts[3][ld] := int(N_A * V * ((c(t_last) - c(0)) * 1e-3)) for
+ * GLC, G6P, LCTS (flux_conversion.millimolar_to_counts), V = volume_fl*1e-15.
+ * h_state (nullable, in/out, hours): step-size carry-over.                  */
+int vk_kremling_step(const vk_kremling_params *params, int64_t n_agents, int64_t ld,
+                     double timestep_h, double grid_h, int32_t n_grid, double rtol, double atol,
+                     int32_t max_steps, double *state, const double *volume_fl, double avogadro,
+                     double *h_state, double *flux, int64_t *counts, int32_t *status,
+                     int32_t *nsteps, vk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,7 +29,7 @@ EXPORTS = (
     'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_field_uniform',
     'vk_diffuse', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites', 'vk_cell_step', 'vk_divide_scratch_bytes', 'vk_divide_plan',
-    'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations',
+    'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations', 'vk_kremling_step',
 )
 
 VK_CELL_MASS, VK_CELL_VOLUME, VK_CELL_LENGTH, VK_CELL_SURFACE_AREA, VK_CELL_PROTEIN, VK_CELL_ANGLE = range(6)
@@ -75,6 +75,13 @@ class VkCellParams(ctypes.Structure):
             'sa_lin')] + [('seed', ctypes.c_uint64), ('step', ctypes.c_uint64)]
 
 
+class VkKremlingParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        'k1', 'k2', 'k3', 'K1', 'K2', 'K3', 'kd', 'm', 'n', 'x0', 'kg6p', 'Kg6p', 'kptsup', 'Kglc',
+        'Keiiap', 'klac', 'Km_lac', 'Kieiia', 'kgly', 'kpyk', 'kpdh', 'kpts', 'km_pts', 'mw1', 'mw2',
+        'mw3', 'Y1_sim', 'Y2_sim', 'Y3_sim', 'K', 'kb', 'ksyn', 'KI')]
+
+
 _SIGS = {
     'vk_abi_version': ([], ctypes.c_int),
     'vk_last_error': ([], ctypes.c_char_p),
@@ -102,6 +109,8 @@ _SIGS = {
     'vk_divide_gather': ([_i64, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp], ctypes.c_int),
     'vk_divide_lineage': ([_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     'vk_divide_locations': ([_i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
+    'vk_kremling_step': ([ctypes.POINTER(VkKremlingParams), _i64, _i64, _f64, _f64, _i32, _f64, _f64, _i32,
+                          _vp, _vp, _f64, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
 }
 
 _lib = None
