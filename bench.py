@@ -53,6 +53,8 @@ def parse():
     p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
+    p.add_argument('--stencil-kernel', type=int, default=3,
+                   help='0 workgroup/LDS, 1 wave/DPP lag-2, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows')
     p.add_argument('--stencil-depth', type=int, default=9)
     p.add_argument('--stencil-rows', type=int, default=64)
     p.add_argument('--no-cpu-baseline', action='store_true')
@@ -89,7 +91,7 @@ def build_rank(args, rank, world, dev):
 
 
 def time_stencil_pass(lat, depth, reps=20):
-    """Average duration of ONE fused pass (k_diffuse_wt<depth>, non-final: fields ->
+    """Average duration of ONE fused pass of `depth` substeps (non-final: fields ->
     work buffer, fields untouched), HIP events on the launch stream."""
     from lens_amd import native
     lo_min = lat.row_lo if lat.edge_top else 0
@@ -169,7 +171,7 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
     from lens_amd.lattice import stencil_depth, stencil_kernel
     stencil_depth(args.stencil_depth)
-    stencil_kernel(1, args.stencil_rows)
+    stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = None
     if world > 1 and lat is not None:
@@ -240,9 +242,13 @@ def main():
                 with open(pmc) as f:
                     rec = json.load(f)
                 # the committed PMC pass must describe this exact launch geometry
-                if (rec.get('depth'), rec.get('rows'), rec.get('cells')) == (depth, args.stencil_rows, cells):
+                if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant')) == (
+                        depth, args.stencil_rows, cells, args.stencil_kernel):
                     traffic = rec.get('hbm_bytes_per_launch')
-            roofline = {'bound': 'hbm', 'kernel': 'k_diffuse_wt<%d, false>' % depth, 'achieved': achieved,
+            kname = ('k_diffuse_wl<%d, %d, false>' % (depth, 3 * (args.stencil_kernel - 1))
+                     if args.stencil_kernel >= 2 else
+                     'k_diffuse_wt<%d, false>' % depth if args.stencil_kernel == 1 else 'k_diffuse_tb<%d>' % depth)
+            roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
                         'traffic': traffic, 'bytes_per_launch': bytes_per_launch,
                         'avg_launch_ms': launch_ms, 'substeps_per_launch': depth,

@@ -19,6 +19,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <utility>
+
 
 #include "vk_internal.h"
 
@@ -354,7 +356,164 @@ __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ s
         diffuse_wt_body<K, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
-static int g_stencil_rows = 128;
+// ---------------------------------------------------------------------------
+// Wave-tile, lag-1 pipeline (variant 2).  Same tile / DPP scheme as
+// k_diffuse_wt, but stage q consumes stage q-1's output of the SAME iteration
+// (stage q computes row i-1-q at iteration i).  At the start of an iteration
+// each stage holds only two live rows (up, centre) instead of three, so the
+// register footprint drops from ~3K to ~2K row-pairs and more waves fit per
+// SIMD; the price is a dependency chain through the stages of one iteration,
+// which the unrolled body and the extra waves overlap.  Slot roles rotate with
+// the iteration phase U (period 3): up = S[U], centre = S[U+1], fresh = S[U+2].
+// ---------------------------------------------------------------------------
+
+// PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
+template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U>
+__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD],
+                                        const double *__restrict__ s, double *__restrict__ d,
+                                        const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    constexpr int R = U % 3;
+    double2(&UP)[K] = R == 0 ? S0 : (R == 1 ? S1 : S2);
+    double2(&CN)[K] = R == 0 ? S1 : (R == 1 ? S2 : S0);
+    double2(&FR)[K] = R == 0 ? S2 : (R == 1 ? S0 : S1);
+    const int64_t ny = L.ny;
+    FR[0] = pf[U];                                                                          // row i
+    pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L);     // row i+PD
+    const int r_out = i - K;
+    const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
+    double2 base = make_double2(0.0, 0.0);
+    if (FINAL && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        // stage q is useful for rows [c0-(K-1-q), c1+(K-1-q)), i.e. i in [c0-K+2+2q, c1+K)
+        if (!STEADY && (i < c0 - K + 2 + 2 * q || i >= c1 + K)) continue;
+        const int r = i - 1 - q;
+        const double2 cen = CN[q];
+        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double2 dn = (EDGE && r == bot_reflect) ? cen : FR[q];
+        double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
+        double rightA = cen.y, leftB = cen.x;
+        if (EDGE) {
+            leftA = L.lA ? cen.x : leftA;
+            rightA = L.rA ? cen.x : rightA;
+            leftB = L.lB ? cen.y : leftB;
+            rightB = L.rB ? cen.y : rightB;
+        }
+        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
+        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
+        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
+        if (q + 1 < K) {
+            FR[q + 1] = v;
+        } else if (row_ok) {
+            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            double *o = d + (int64_t)r_out * ny + L.cA;
+            if (!EDGE) {
+                if (L.wA) *reinterpret_cast<double2 *>(o) = v;
+            } else {
+                if (L.wA) o[0] = v.x;
+                if (L.wB) o[1] = v.y;
+            }
+        }
+    }
+}
+
+template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U0, int... Us>
+__device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
+                                         double2 (&pf)[PD], const double *__restrict__ s, double *__restrict__ d,
+                                         const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect,
+                                        bot_reflect, coef);
+    if constexpr (sizeof...(Us) > 0)
+        wl_group<K, PD, EDGE, FINAL, STEADY, Us...>(S0, S1, S2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi,
+                                                top_reflect, bot_reflect, coef);
+}
+
+template <int K, int PD, bool EDGE, bool FINAL, int... Us>
+__device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
+                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD],
+                                                const double *__restrict__ s, double *__restrict__ d,
+                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                                double coef) {
+    const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
+    const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
+#define WL_ARGS S0, S1, S2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef
+    int i = i0;
+    for (; i + PD <= i1 && i < s_lo; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);   // fill
+    for (; i + PD - 1 <= s_hi; i += PD) wl_group<K, PD, EDGE, FINAL, true, Us...>(WL_ARGS);          // steady
+    for (; i + PD <= i1; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);               // drain
+    // tail: fewer than PD iterations, phases 0.. in order
+    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, false, Us>(S0, S1, S2, pf, s, d, g, L, i + Us, c0, c1, in_lo,
+                                                        in_hi, top_reflect, bot_reflect, coef)
+                  : void()), ...);
+#undef WL_ARGS
+}
+
+template <int K, int PD, bool EDGE, bool FINAL>
+__device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *__restrict__ d,
+                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                                double coef) {
+    double2 S0[K], S1[K], S2[K], pf[PD];
+#pragma unroll
+    for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
+    const int64_t ny = L.ny;
+    const int i0 = c0 - K + 2;
+    // stage 0's window before the first iteration: up = row i0-2, centre = row i0-1
+    S0[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 2, in_lo), in_hi - 1) * ny, L);
+    S1[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 1, in_lo), in_hi - 1) * ny, L);
+#pragma unroll
+    for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
+    diffuse_wl_loop<K, PD, EDGE, FINAL>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, s, d, g, L, c0, c1,
+                                    in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+template <int K, int PD, bool FINAL>
+__global__ __launch_bounds__(256) void k_diffuse_wl(const double *__restrict__ src, double *__restrict__ dst,
+                                                    const double *__restrict__ f0, int64_t field_stride, int ny,
+                                                    int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
+                                                    int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
+                                                    int n_fields, double coef, const double *__restrict__ uniform) {
+    constexpr int KH = K + (K & 1);
+    constexpr int W = WT_COLS - 2 * KH;
+    // (An XCD-contiguous tile order -- each XCD's L2 serving its tiles' shared
+    // halo columns -- measured 4 % slower on 4096^2: the halo re-reads already
+    // hit the die-level Infinity Cache, so plain round-robin order is kept.)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int lane = threadIdx.x & 63;
+    if (wave >= tiles_x * chunks_y * n_fields) return;
+    const int tx = wave % tiles_x;
+    const int ty = (wave / tiles_x) % chunks_y;
+    const int f = wave / (tiles_x * chunks_y);
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;
+    const int c0 = out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = tx * W;
+    WtLane L;
+    L.ny = ny;
+    L.cA = x0 - KH + 2 * lane;
+    const int cB = L.cA + 1;
+    L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
+    L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
+    L.lA = L.cA == 0;
+    L.rA = L.cA == ny - 1;
+    L.lB = cB == 0;
+    L.rB = cB == ny - 1;
+    const double *s = src + (int64_t)f * field_stride;
+    double *d = dst + (int64_t)f * field_stride;
+    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
+                      (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
+                      (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
+    if (edge)
+        diffuse_wl_body<K, PD, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    else
+        diffuse_wl_body<K, PD, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+static int g_stencil_rows = 64;
 
 template <int K>
 static void launch_wt(hipStream_t st, const double *src, double *dst, const double *f0, int nf, int64_t fs,
@@ -374,7 +533,37 @@ static void launch_wt(hipStream_t st, const double *src, double *dst, const doub
                            out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
 }
 
-static int g_stencil_kernel = 1;  // 0 = workgroup tile (LDS exchange), 1 = wave tile (DPP)
+static int g_stencil_kernel = 3;  // 0 = workgroup tile (LDS), 1 = wave tile (DPP), 2/3/4 = wave tile lag-1, prefetch 3/6/9 rows
+
+template <int K, int PD>
+static void launch_wl(hipStream_t st, const double *src, double *dst, const double *f0, int nf, int64_t fs,
+                      int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot, double coef,
+                      const double *mm) {
+    constexpr int KH = K + (K & 1);
+    constexpr int W = WT_COLS - 2 * KH;
+    const int rch = g_stencil_rows;
+    const int tiles_x = (ny + W - 1) / W;
+    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
+    const int waves = tiles_x * chunks_y * nf;
+    if (f0)
+        hipLaunchKernelGGL((k_diffuse_wl<K, PD, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs,
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+    else
+        hipLaunchKernelGGL((k_diffuse_wl<K, PD, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs,
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+}
+
+template <int PD>
+static void launch_wl_k(int k, hipStream_t st, const double *src, double *dst, const double *f0, int nf,
+                        int64_t fs, int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot,
+                        double coef, const double *mm) {
+#define VK_WL(KC) case KC: launch_wl<KC, PD>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm); break
+    switch (k) {
+        VK_WL(3); VK_WL(5); VK_WL(7); VK_WL(9); VK_WL(11); VK_WL(13); VK_WL(15);
+        default: break;
+    }
+#undef VK_WL
+}
 
 static void launch_wt_k(int k, hipStream_t st, const double *src, double *dst, const double *f0, int nf,
                         int64_t fs, int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot,
@@ -389,12 +578,12 @@ static void launch_wt_k(int k, hipStream_t st, const double *src, double *dst, c
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 0 || variant == 1) g_stencil_kernel = variant;
+    if (variant >= 0 && variant <= 4) g_stencil_kernel = variant;
     if (rows >= 8 && rows <= 4096) g_stencil_rows = rows;
     return prev;
 }
 
-static int g_stencil_depth = 15;  // substeps per HBM pass (odd; 1 = one launch per substep)
+static int g_stencil_depth = 9;   // max substeps per HBM pass (odd; 1 = one launch per substep)
 
 extern "C" int vk_set_stencil_depth(int32_t k) {
     const int prev = g_stencil_depth;
@@ -460,9 +649,17 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
     const int last_in_call = sub_begin + sub_count - 1;
     int depth = g_stencil_depth | 1;   // odd
     if (depth > 15) depth = 15;
-    for (int j = sub_begin; j <= last_in_call;) {
-        int k = std::min(depth, last_in_call - j + 1);
-        if ((k & 1) == 0) k -= 1;   // even remainder: odd pass now, the rest next
+    // Pass plan: the fewest odd depths <= depth that sum to sub_count (a sum of
+    // P odd numbers has the parity of P), as even as possible -- e.g. 100 =
+    // 8x9 + 4x7 rather than 11x9 + a lone single-substep pass.
+    int passes = (sub_count + depth - 1) / depth;
+    if ((passes & 1) != (sub_count & 1)) ++passes;
+    for (int j = sub_begin, left = passes; j <= last_in_call; --left) {
+        const int rem = last_in_call - j + 1;   // rem has the parity of `left`
+        int k = (rem + left - 1) / left;
+        if ((k & 1) == 0) ++k;
+        if (k > depth) k = depth;
+        while (k > 1 && rem - k < left - 1) k -= 2;
         const int e = j + k - 1;     // last substep of this pass
         const int grow = last_in_call - e;
         const int lo = max(lo_min, row_lo - grow);
@@ -479,6 +676,10 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform);
+        } else if (g_stencil_kernel >= 2) {
+            auto launch = g_stencil_kernel == 2 ? launch_wl_k<3> : (g_stencil_kernel == 3 ? launch_wl_k<6> : launch_wl_k<9>);
+            launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
+                   coeff_dt, uniform);
         } else if (g_stencil_kernel == 1) {
             launch_wt_k(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
                         bot_reflect, coeff_dt, uniform);
@@ -527,9 +728,20 @@ constexpr int UN_PER_THREAD = 8;
 __global__ __launch_bounds__(256) void k_uniform_probe(const double *__restrict__ fields, int64_t field_stride,
                                                        int64_t off, int64_t count, double *sum) {
     const int f = blockIdx.y;
-    volatile double *vs = sum + 2 * f;
-    const double v0 = vs[0];
-    if (!(v0 == vs[1])) return;                       // already non-uniform (or NaN)
+    double *vs = sum + 2 * f;
+    // one lane per block reads the summary (every lane polling one address
+    // serialises on a single L2 channel), the block shares it through LDS
+    __shared__ double s_v0;
+    __shared__ int s_done;
+    if (threadIdx.x == 0) {
+        const double lo = __hip_atomic_load(vs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double hi = __hip_atomic_load(vs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_v0 = lo;
+        s_done = !(lo == hi);                         // already non-uniform (or NaN)
+    }
+    __syncthreads();
+    if (s_done) return;
+    const double v0 = s_v0;
     const double *p = fields + (int64_t)f * field_stride + off;
     const int64_t base = (int64_t)blockIdx.x * (256 * UN_PER_THREAD) + threadIdx.x;
     bool diff = false;
@@ -539,8 +751,8 @@ __global__ __launch_bounds__(256) void k_uniform_probe(const double *__restrict_
         if (i < count) diff |= !(p[i] == v0);
     }
     if (__syncthreads_or(diff) && threadIdx.x == 0) {
-        vs[0] = -INFINITY;
-        vs[1] = INFINITY;
+        __hip_atomic_store(vs, -INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(vs + 1, INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

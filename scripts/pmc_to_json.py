@@ -1,7 +1,7 @@
 """Fold rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) for one stencil kernel into
 profiles/pmc_stencil.json, which bench.py reads for roofline.traffic.
 
-    python scripts/pmc_to_json.py KERNEL CELLS DEPTH ROWS fetch.csv write.csv [out.json]
+    python scripts/pmc_to_json.py KERNEL CELLS DEPTH ROWS VARIANT fetch.csv write.csv [out.json]
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a wide
@@ -21,12 +21,12 @@ def mean_counter(path, kernel, counter):
     return sum(vals) / len(vals), len(vals)
 
 
-kernel, cells, depth, rows, fcsv, wcsv = sys.argv[1:7]
-out = sys.argv[7] if len(sys.argv) > 7 else 'profiles/pmc_stencil.json'
+kernel, cells, depth, rows, variant, fcsv, wcsv = sys.argv[1:8]
+out = sys.argv[8] if len(sys.argv) > 8 else 'profiles/pmc_stencil.json'
 fetch_kib, nf = mean_counter(fcsv, kernel, 'FETCH_SIZE')
 write_kib, nw = mean_counter(wcsv, kernel, 'WRITE_SIZE')
 rec = {
-    'kernel': kernel, 'cells': int(cells), 'depth': int(depth), 'rows': int(rows),
+    'kernel': kernel, 'cells': int(cells), 'depth': int(depth), 'rows': int(rows), 'variant': int(variant),
     'fetch_size_kib': fetch_kib, 'write_size_kib': write_kib, 'dispatches': [nf, nw],
     'read_bytes_per_launch': 2.0 * fetch_kib * 1024.0,
     'write_bytes_per_launch': write_kib * 1024.0,

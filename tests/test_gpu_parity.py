@@ -291,7 +291,9 @@ def test_dopri5_wave_equals_lane_variant_small_network(dev):
     assert np.mean(out[0][1] == out[1][1]) > 0.99
 
 
-@pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (1, 3), (1, 7), (1, 11), (1, 15)])
+@pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (1, 3), (1, 7), (1, 11), (1, 15),
+                                           (2, 3), (2, 5), (2, 9), (2, 13), (2, 15), (3, 7), (3, 9),
+                                           (4, 5), (4, 11)])
 def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
     """Every kernel variant and temporal-blocking depth reproduces
     scipy.ndimage.convolve bit for bit."""
@@ -316,7 +318,9 @@ def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
 
 
 @pytest.mark.parametrize('variant,depth,rows', [(0, 15, 64), (1, 15, 64), (1, 5, 256), (1, 9, 128),
-                                                (1, 13, 32), (1, 7, 512)])
+                                                (1, 13, 32), (1, 7, 512), (2, 9, 64), (2, 7, 128),
+                                                (2, 11, 32), (2, 15, 256), (3, 9, 64), (3, 13, 48),
+                                                (4, 9, 96), (4, 7, 40)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
 def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
     """Multi-tile / multi-chunk geometry: interior tiles, ragged last tile and
