@@ -39,6 +39,9 @@ WORKLOADS = {
     'c4': (1_000_000, 4096, 4096.0, 'BASELINE config 4: 1M agents + 4096x4096 diffusion_field lattice'),
     'c3': (100_000, 1024, 1024.0, 'BASELINE config 3: 100k agents + 1024x1024 diffusion_field lattice'),
     'c2': (10_000, 0, 0.0, 'BASELINE config 2: 10k heterogeneous agents, no lattice'),
+    'c5': (1_000_000, 0, 0.0, 'BASELINE config 5: 50-species / 40-reaction network per agent (~85 integrated '
+                              'components, agent-per-wavefront DP45) + Growth/DeriveGlobals/DivisionVolume '
+                              'division events'),
 }
 
 
@@ -64,7 +67,13 @@ def parse():
 
 def build_rank(args, rank, world, dev):
     n_total, nx, bound, _ = WORKLOADS[args.workload]
-    cfg = configs.glc_ac_config() if nx else configs.glc_lct_config()
+    cells = None
+    if args.workload == 'c5':
+        from lens_amd.cells import CellModel
+        cfg = configs.synthetic_network(n_species=50, n_reactions=40, n_enzymes=10)
+        cells = CellModel(model='growth', growth_rate=0.0006, division_volume=2.4)
+    else:
+        cfg = configs.glc_ac_config() if nx else configs.glc_lct_config()
     table = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
     rng = np.random.default_rng(configs.SEED + rank)
     lat = None
@@ -81,10 +90,15 @@ def build_rank(args, rank, world, dev):
         loc = np.stack([x, y])
     else:
         n_local = n_total // world + (1 if rank < n_total % world else 0)
-    params, conc = configs.heterogeneous_colony(table, cfg, n_local, seed=configs.SEED + rank)
+    params, conc = configs.heterogeneous_colony(table, cfg, n_local, seed=configs.SEED + rank,
+                                                sigma=0.2 if cells is not None else 0.25)
     col = Colony(cfg, n_local, device=dev, integrator=args.integrator, environment=lat or 'held',
-                 table=table, exchange=args.exchange, specialize=not args.generic_kernel)
+                 table=table, exchange=args.exchange, specialize=not args.generic_kernel, cells=cells,
+                 capacity=int(n_local * 1.05) + 64 if cells is not None else None)
     col.set_agents(params=params, conc=conc, location=loc if nx else None)
+    if cells is not None:
+        # a colony spread over one generation: divisions every step from the start
+        col.set_cell_mass(rng.uniform(1339.0, 2.4 * 1100.0, n_local))
     if nx:
         col.gather_external()
     return col, lat, (params, conc, loc if nx else None)
@@ -123,10 +137,15 @@ def cpu_baseline(args, col, host_state):
     os.environ.setdefault('OMP_NUM_THREADS', str(threads))
     cpu.build()
     params, conc, loc = host_state
-    conc = conc.copy()
     t = col.table
     desc = cpu.Desc(t)
     n = conc.shape[1]
+    if col.lattice is None and n > 4096:
+        # no lattice: agents are independent -> a bounded sample of them, scaled per agent
+        n = 4096
+        params = np.ascontiguousarray(params[:, :n])
+        conc = np.ascontiguousarray(conc[:, :n])
+    conc = conc.copy()
     m2c = col.m2c[:n].cpu().numpy().copy()
     h = np.zeros(n)
     lat = col.lattice
@@ -149,13 +168,14 @@ def cpu_baseline(args, col, host_state):
                 cpu.exchange(fields[fi].reshape(-1), bin_lin, counts[e], lat.binvol_avogadro)
         steps += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or steps >= 20:
+        if el >= args.cpu_seconds or steps >= 20 or (fields is None and el >= args.cpu_seconds / 3):
             break
     return {'value': steps * n / el, 'unit': 'agent-steps/s', 'cores': threads, 'kind': 'port',
-            'sample': '%d full step(s) of the same %d-agent workload (DP45 kinetics%s), %.1f s, '
-                      'oracle/cpu_kinetics.c with OpenMP' % (
+            'sample': '%d full step(s) of %d agents of the same workload (DP45 kinetics%s), %.1f s, '
+                      'oracle/cpu_kinetics.c with OpenMP%s' % (
                           steps, n, ' + 100-substep stencil x %d fields + exchange' % len(fields)
-                          if fields is not None else '', el)}
+                          if fields is not None else '', el,
+                          '; growth/division not included (negligible work)' if col.cells is not None else '')}
 
 
 def main():
@@ -195,9 +215,12 @@ def main():
     barrier()
     col.check_status()
     nsteps_acc.zero_()
+    agent_steps = 0          # agents integrated, summed over the timed steps (divisions grow n)
+    n_start = col.n
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
+        agent_steps += col.n
         col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing[k])
         nsteps_acc += col.nsteps[:col.n].sum()
     barrier()
@@ -205,7 +228,7 @@ def main():
     col.check_status()
     stencil_pass_ms = time_stencil_pass(lat, args.stencil_depth) if lat is not None else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    n_agents = torch.tensor([float(col.n)], dtype=torch.float64, device=dev)
+    n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
     kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
     diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
                if lat is not None else 0.0)
@@ -214,15 +237,16 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(n_agents, op=dist.ReduceOp.SUM)
     elapsed = float(el.item())
-    total_agents = float(n_agents.item())
-    value = total_agents * args.steps / elapsed
+    total_agent_steps = float(n_agents.item())
+    value = total_agent_steps / elapsed
 
     if rank == 0:
         n_total, nx, bound, desc = WORKLOADS[args.workload]
         integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
-        integ = {'kernel': 'vk_dopri5_spec' if col.engine.specialized else 'k_dopri5_thread',
-                 'avg_ms_per_step': kin_ms,
-                 'dp45_attempts_per_agent_step': attempts / args.steps / col.n,
+        variant = col.engine.default_variant()
+        kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec'}[variant]
+        integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
+                 'dp45_attempts_per_agent_step': attempts / agent_steps,
                  'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),
                  'achieved_tflops': integ_flops / (kin_ms * 1e-3) / 1e12 if kin_ms else None,
                  'peak_tflops': FP64_PEAK_TFLOPS}
@@ -257,7 +281,7 @@ def main():
                         'fp64_frac': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                         'step_diffusion_ms': diff_ms}
         else:
-            roofline = {'bound': 'fp64-valu', 'kernel': 'k_dopri5_thread',
+            roofline = {'bound': 'fp64-valu', 'kernel': kname_i,
                         'achieved': integ.get('achieved_tflops'), 'peak': FP64_PEAK_TFLOPS,
                         'unit': 'TFLOP/s', 'frac': integ.get('frac'), 'traffic': None}
         out = {
@@ -266,6 +290,7 @@ def main():
             'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (seeded heterogeneous colony, SURVEY.md §8d distributions)',
             'config': {'workload': desc, 'agents': n_total, 'lattice': [nx, nx] if nx else None,
+                       'agents_end': col.n if world == 1 else None, 'agents_start': n_start if world == 1 else None,
                        'fields': lat.molecules if lat is not None else None, 'dt_s': 1.0,
                        'substeps_per_step': n_substeps(1.0) if nx else 0,
                        'integrator': args.integrator, 'rtol': col.rtol, 'atol': col.atol,

@@ -225,6 +225,18 @@ class Colony:
         self.time += dt
         self.step_index += 1
 
+    def set_cell_mass(self, mass):
+        """Per-agent masses (fg) for agents 0..n-1 with their derived volume,
+        length, surface area and mmol_to_counts (DeriveGlobals on each)."""
+        cm = self.cells
+        mass = np.ascontiguousarray(mass, dtype=np.float64)[:self.n]
+        vol, m2c, length, area = cm.derive(mass)          # numpy: the same IEEE ops elementwise
+        rows = self.cell[:, :self.n].cpu().numpy()
+        rows[native.VK_CELL_MASS], rows[native.VK_CELL_VOLUME] = mass, vol
+        rows[native.VK_CELL_LENGTH], rows[native.VK_CELL_SURFACE_AREA] = length, area
+        self.cell[:, :self.n].copy_(torch.from_numpy(rows))
+        self.m2c[:self.n].copy_(torch.from_numpy(np.ascontiguousarray(m2c)))
+
     # -- growth, derivers, division (a10-a13) ------------------------------------
     def grow_and_divide(self, dt: float):
         """Growth process + TreeMass/DeriveGlobals, then division.  Returns the

@@ -27,6 +27,7 @@ struct vk_table {
     vk_dev_table dev;
     void *blob;  // single device allocation holding every array
     int32_t n_sets, n_members, n_upd, n_exch;
+    int32_t n_ib, n_db;                    // element counts of the int / double blob parts
     hipModule_t spec_module = nullptr;     // vk_table_specialize (hiprtc)
     hipFunction_t spec_dopri5 = nullptr;
 };

@@ -149,6 +149,7 @@ extern "C" int vk_table_create(const vk_table_desc *d, vk_table **out) {
     vk_table *t = new vk_table();
     t->blob = blob;
     t->n_sets = d->n_sets; t->n_members = d->n_members; t->n_upd = d->n_upd; t->n_exch = d->n_exch;
+    t->n_ib = (int32_t)ints.size(); t->n_db = (int32_t)dbl.size();
     vk_dev_table &v = t->dev;
     v.ib = ibase;
     v.db = (const double *)blob;
@@ -614,8 +615,10 @@ __global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t
 // Dormand-Prince 5(4), agent per WAVEFRONT (networks too large for a lane)
 // ---------------------------------------------------------------------------
 //
-// One 64-lane wavefront integrates one agent (one wave per workgroup, so
-// __syncthreads() is a wave barrier).  Component i of y = [dyn species |
+// One 64-lane wavefront integrates one agent; a workgroup of 4 waves stages
+// the (shared, read-only) rate-law table into LDS once, then each wave runs its
+// own agent with wave-local synchronisation only (waves take different numbers
+// of steps, so no block barrier after staging).  Component i of y = [dyn species |
 // flux integrals] lives in lane i % 64, slot i / 64 (NSLOT slots per lane).
 // Each RHS: lanes publish their species to the agent's LDS tile, lane l
 // evaluates rate laws l, l+64, ... (same arithmetic as rate_law_tile), lane r
@@ -626,6 +629,15 @@ __global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t
 // norm's sum differs).
 
 constexpr int DW = 64;
+constexpr int DW_WAVES = 4;   // agents (waves) per workgroup
+
+// LDS communication between the lanes of ONE wave: a wave's LDS operations
+// execute in order, so only the compiler must be kept from reordering.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -635,8 +647,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // rate law l from the agent's LDS tile (cl: species, pl: kcat or 1/Km);
 // table indices are lane-divergent here, so they are plain (vector) loads
-__device__ __forceinline__ double rate_law_wave(const vk_dev_table &t, int l, const double *cl, const double *pl) {
-    const int32_t *ib = t.ib;
+__device__ __forceinline__ double rate_law_wave(const vk_dev_table &t, const int32_t *ib, int l, const double *cl,
+                                                const double *pl) {
     double num = 0.0;
     const int ns0 = ib[t.o_rl_num_ptr + l], ns1 = ib[t.o_rl_num_ptr + l + 1];
     const double kcat = pl[ib[t.o_rl_kcat + l]];
@@ -659,37 +671,37 @@ __device__ __forceinline__ double rate_law_wave(const vk_dev_table &t, int l, co
 }
 
 template <int NSLOT>
-__device__ __forceinline__ void rhs_wave(const vk_dev_table &t, const double (&y)[NSLOT], double (&dy)[NSLOT],
-                                         double *cl, double *fl, const double *pl, double *rl, int lane) {
+__device__ __forceinline__ void rhs_wave(const vk_dev_table &t, const int32_t *ib, const double *db,
+                                         const double (&y)[NSLOT], double (&dy)[NSLOT], double *cl, double *fl,
+                                         const double *pl, double *rl, int lane) {
     const int nd = t.n_dyn, nr = t.n_reactions, nl = t.n_rate_laws;
-    const int32_t *ib = t.ib;
 #pragma unroll
     for (int k = 0; k < NSLOT; ++k) {
         const int i = lane + DW * k;
         if (i < nd) cl[i] = y[k];
     }
-    __syncthreads();
-    for (int l = lane; l < nl; l += DW) rl[l] = rate_law_wave(t, l, cl, pl);
-    __syncthreads();
+    wave_sync();
+    for (int l = lane; l < nl; l += DW) rl[l] = rate_law_wave(t, ib, l, cl, pl);
+    wave_sync();
     for (int r = lane; r < nr; r += DW) {
         double f = 0.0;
         for (int k = ib[t.o_rx_ptr + r]; k < ib[t.o_rx_ptr + r + 1]; ++k) f += rl[ib[t.o_rx_rl + k]];
         fl[r] = f;
     }
-    __syncthreads();
+    wave_sync();
 #pragma unroll
     for (int k = 0; k < NSLOT; ++k) {
         const int i = lane + DW * k;
         double d = 0.0;
         if (i < nd) {
             for (int j = ib[t.o_upd_ptr + i]; j < ib[t.o_upd_ptr + i + 1]; ++j)
-                d = fma(t.db[t.o_upd_coeff + j], fl[ib[t.o_upd_rxn + j]], d);
+                d = fma(db[t.o_upd_coeff + j], fl[ib[t.o_upd_rxn + j]], d);
         } else if (i < nd + nr) {
             d = fl[i - nd];
         }
         dy[k] = d;
     }
-    __syncthreads();   // the next RHS overwrites cl / fl
+    wave_sync();   // the next RHS overwrites cl / fl
 }
 
 template <int NSLOT>
@@ -706,34 +718,45 @@ __device__ __forceinline__ double wave_rms(const double (&v)[NSLOT], const doubl
 }
 
 template <int NSLOT>
-__global__ __launch_bounds__(DW) void k_dopri5_wave(vk_dev_table t, int64_t n, int64_t ld, double dt, double rtol,
-                                                    double atol, int max_steps, const double *__restrict__ params,
-                                                    double *__restrict__ conc, const double *__restrict__ m2c,
-                                                    double *__restrict__ delta, double *__restrict__ h_state,
-                                                    double *__restrict__ flux, int64_t *__restrict__ counts,
-                                                    int32_t *__restrict__ status, int32_t *__restrict__ nsteps_out) {
+__global__ __launch_bounds__(DW * DW_WAVES) void k_dopri5_wave(vk_dev_table t, int n_ib, int n_db, int tile,
+                                                               int64_t n, int64_t ld, double dt, double rtol,
+                                                               double atol, int max_steps,
+                                                               const double *__restrict__ params,
+                                                               double *__restrict__ conc,
+                                                               const double *__restrict__ m2c,
+                                                               double *__restrict__ delta,
+                                                               double *__restrict__ h_state,
+                                                               double *__restrict__ flux,
+                                                               int64_t *__restrict__ counts,
+                                                               int32_t *__restrict__ status,
+                                                               int32_t *__restrict__ nsteps_out) {
     extern __shared__ double lds[];
-    const int lane = threadIdx.x;
-    const int64_t a = blockIdx.x;
+    // [table doubles | table ints | one agent tile per wave]
+    double *db = lds;
+    int32_t *ib = (int32_t *)(lds + n_db);
+    for (int i = threadIdx.x; i < n_db; i += DW * DW_WAVES) db[i] = t.db[i];
+    for (int i = threadIdx.x; i < n_ib; i += DW * DW_WAVES) ib[i] = t.ib[i];
+    __syncthreads();   // the only block barrier: waves run independent agents from here on
+    const int lane = threadIdx.x & (DW - 1), w = threadIdx.x / DW;
+    const int64_t a = (int64_t)blockIdx.x * DW_WAVES + w;
     if (a >= n) return;
     const int ns_ = t.n_species, nr = t.n_reactions, np_ = t.n_params, nd = t.n_dyn;
     const int ny = nd + nr;
-    double *cl = lds;                 // [n_species]
+    double *cl = lds + n_db + (n_ib + 1) / 2 + (int64_t)w * tile;   // [n_species]
     double *fl = cl + ns_;            // [n_reactions]
     double *pl = fl + nr;             // [n_params]  kcat or 1/Km
     double *rl = pl + np_;            // [n_rate_laws]
-    const int32_t *ib = t.ib;
 
     for (int s = lane; s < ns_; s += DW) cl[s] = conc[(int64_t)s * ld + a];
     for (int p = lane; p < np_; p += DW) pl[p] = params[(int64_t)p * ld + a];
-    __syncthreads();
+    wave_sync();
     const int n_mem = ib[t.o_set_ptr + ib[t.o_rl_den_ptr + t.n_rate_laws]];
     for (int m = lane; m < n_mem; m += DW) {
         const int p = ib[t.o_mem_param + m];
         const double km = params[(int64_t)p * ld + a];
         pl[p] = (km != 0.0) ? 1.0 / km : 0.0;
     }
-    __syncthreads();
+    wave_sync();
 
     double y[NSLOT], k1[NSLOT], k2[NSLOT], k3[NSLOT], k4[NSLOT], k5[NSLOT], k6[NSLOT], k7[NSLOT], yt[NSLOT];
 #pragma unroll
@@ -741,7 +764,7 @@ __global__ __launch_bounds__(DW) void k_dopri5_wave(vk_dev_table t, int64_t n, i
         const int i = lane + DW * k;
         y[k] = (i < nd) ? cl[i] : 0.0;
     }
-    rhs_wave<NSLOT>(t, y, k1, cl, fl, pl, rl, lane);
+    rhs_wave<NSLOT>(t, ib, db, y, k1, cl, fl, pl, rl, lane);
     int32_t st = 0;
     double h = h_state ? h_state[a] : 0.0;
     if (!(h > 0.0)) {   // scipy select_initial_step (order 4)
@@ -753,7 +776,7 @@ __global__ __launch_bounds__(DW) void k_dopri5_wave(vk_dev_table t, int64_t n, i
         h0 = fmin(h0, dt);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k) yt[k] = fma(h0, k1[k], y[k]);
-        rhs_wave<NSLOT>(t, yt, k2, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k2, cl, fl, pl, rl, lane);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k) k2[k] = k2[k] - k1[k];
         const double d2 = wave_rms<NSLOT>(k2, sc, lane, ny) / h0;
@@ -773,28 +796,28 @@ __global__ __launch_bounds__(DW) void k_dopri5_wave(vk_dev_table t, int64_t n, i
         ++nsteps;
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k) yt[k] = fma(hs, dp::a21 * k1[k], y[k]);
-        rhs_wave<NSLOT>(t, yt, k2, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k2, cl, fl, pl, rl, lane);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k) yt[k] = fma(hs, fma(dp::a32, k2[k], dp::a31 * k1[k]), y[k]);
-        rhs_wave<NSLOT>(t, yt, k3, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k3, cl, fl, pl, rl, lane);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k)
             yt[k] = fma(hs, fma(dp::a43, k3[k], fma(dp::a42, k2[k], dp::a41 * k1[k])), y[k]);
-        rhs_wave<NSLOT>(t, yt, k4, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k4, cl, fl, pl, rl, lane);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k)
             yt[k] = fma(hs, fma(dp::a54, k4[k], fma(dp::a53, k3[k], fma(dp::a52, k2[k], dp::a51 * k1[k]))), y[k]);
-        rhs_wave<NSLOT>(t, yt, k5, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k5, cl, fl, pl, rl, lane);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k)
             yt[k] = fma(hs, fma(dp::a65, k5[k], fma(dp::a64, k4[k], fma(dp::a63, k3[k],
                         fma(dp::a62, k2[k], dp::a61 * k1[k])))), y[k]);
-        rhs_wave<NSLOT>(t, yt, k6, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k6, cl, fl, pl, rl, lane);
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k)
             yt[k] = fma(hs, fma(dp::b6, k6[k], fma(dp::b5, k5[k], fma(dp::b4, k4[k],
                         fma(dp::b3, k3[k], dp::b1 * k1[k])))), y[k]);
-        rhs_wave<NSLOT>(t, yt, k7, cl, fl, pl, rl, lane);
+        rhs_wave<NSLOT>(t, ib, db, yt, k7, cl, fl, pl, rl, lane);
         double e2 = 0.0;
 #pragma unroll
         for (int k = 0; k < NSLOT; ++k) {
@@ -839,14 +862,14 @@ __global__ __launch_bounds__(DW) void k_dopri5_wave(vk_dev_table t, int64_t n, i
             flux[(int64_t)(i - nd) * ld + a] = y[k] / dt;
         }
     }
-    __syncthreads();
+    wave_sync();
     if (__any(bad)) st |= VK_AGENT_NONFINITE;
     const double mc = m2c[a];
     int32_t cst = 0;
     for (int e = lane; e < t.n_ext; e += DW) {
         int64_t c = 0;
         for (int j = ib[t.o_ex_ptr + e]; j < ib[t.o_ex_ptr + e + 1]; ++j)
-            c += trunc_count((t.db[t.o_ex_coeff + j] * fl[ib[t.o_ex_rxn + j]]) * mc, cst);
+            c += trunc_count((db[t.o_ex_coeff + j] * fl[ib[t.o_ex_rxn + j]]) * mc, cst);
         counts[(int64_t)e * ld + a] = c;
     }
     if (__any(cst != 0)) st |= VK_AGENT_NONFINITE;
@@ -863,17 +886,23 @@ static int launch_dopri5_wave(const vk_table *t, int64_t n, int64_t ld, double d
                               double *h_state, double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
                               hipStream_t stream) {
     const vk_dev_table &d = t->dev;
-    const size_t lds = (size_t)(d.n_species + d.n_reactions + d.n_params + d.n_rate_laws) * sizeof(double);
-    if (lds > 64 * 1024) {
-        vk::set_error("vk_step_dopri5: network needs %zu B of LDS per agent (> 64 KiB)", lds);
+    const int tile = d.n_species + d.n_reactions + d.n_params + d.n_rate_laws;   // doubles per agent
+    const size_t lds = ((size_t)t->n_db + (t->n_ib + 1) / 2 + (size_t)DW_WAVES * tile) * sizeof(double);
+    if (lds > 160 * 1024) {
+        vk::set_error("vk_step_dopri5: network needs %zu B of LDS per workgroup (> 160 KiB)", lds);
         return VK_ERR_LIMIT;
     }
-    if (n > 0x7fffffff) {
-        vk::set_error("vk_step_dopri5: agent-per-wavefront grid limited to 2^31-1 agents");
+    if (n > 0x1fffffff) {
+        vk::set_error("vk_step_dopri5: agent-per-wavefront grid limited to 2^29 agents");
         return VK_ERR_LIMIT;
     }
-    hipLaunchKernelGGL(k_dopri5_wave<NSLOT>, dim3((unsigned)n), dim3(DW), lds, stream, d, n, ld, dt, o->rtol,
-                       o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux, counts, status, nsteps);
+    if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void *)k_dopri5_wave<NSLOT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024);
+    const unsigned blocks = (unsigned)((n + DW_WAVES - 1) / DW_WAVES);
+    hipLaunchKernelGGL(k_dopri5_wave<NSLOT>, dim3(blocks), dim3(DW * DW_WAVES), lds, stream, d, t->n_ib, t->n_db,
+                       tile, n, ld, dt, o->rtol, o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux,
+                       counts, status, nsteps);
     return vk::launch_check("k_dopri5_wave");
 }
 
