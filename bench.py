@@ -52,14 +52,17 @@ def parse():
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--workload', default='c4', choices=sorted(WORKLOADS))
     p.add_argument('--integrator', default='dopri5', choices=['dopri5', 'euler'])
-    p.add_argument('--halo', type=int, default=10, help='halo depth = substeps per halo exchange')
+    p.add_argument('--halo', type=int, default=50,
+                   help='halo depth = substeps per halo exchange (multi-GPU; scripts/rank_emulate.py: '
+                        '50 beats 25 / 10 on 512-row bands)')
     p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
     p.add_argument('--stencil-kernel', type=int, default=3,
                    help='0 workgroup/LDS, 1 wave/DPP lag-2, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows')
     p.add_argument('--stencil-depth', type=int, default=9)
-    p.add_argument('--stencil-rows', type=int, default=64)
+    p.add_argument('--stencil-rows', type=int, default=None,
+                   help='output rows per wave tile (default 64 on one GPU, 0 = auto on row bands)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -191,6 +194,8 @@ def main():
         dist.init_process_group('nccl', device_id=dev)
     from lens_amd.lattice import stencil_depth, stencil_kernel
     stencil_depth(args.stencil_depth)
+    if args.stencil_rows is None:
+        args.stencil_rows = 64 if world == 1 else 0
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = None

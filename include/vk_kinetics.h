@@ -161,10 +161,11 @@ int vk_step_dopri5(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
  * summary[2f] == summary[2f+1] iff plane f holds a single value (both then
  * hold it); otherwise summary = (-inf, +inf) (a NaN plane is non-uniform).
  * Element-wise min of [2f] / max of [2f+1] over ranks gives the global test.
- * Early exit: cost is ~O(1) for a non-uniform plane.                       */
+ * A non-uniform plane costs one 16-KiB chunk per probe block.              */
+#define VK_UNIFORM_BLOCKS 512   /* scratch: n_fields * VK_UNIFORM_BLOCKS int32 */
 int vk_field_uniform(const double *fields, int32_t n_fields, int64_t field_stride,
                      int32_t ny, int32_t row_lo, int32_t row_hi, double *summary,
-                     vk_stream_t stream);
+                     int32_t *scratch, vk_stream_t stream);
 
 /* Substeps [sub_begin, sub_begin+sub_count) of an n_sub-substep diffusion.
  * Substep j reads src(j) and writes dst(j):
@@ -182,15 +183,19 @@ int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
                const double *uniform, vk_stream_t stream);
 
-/* Substeps fused per HBM pass by vk_diffuse (temporal blocking; odd, 1..15;
- * 1 = one launch per substep).  Returns the previous value; k outside 1..15
- * only queries.  Results are bit-identical for every depth.               */
+/* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
+ * 1..15; 1 = one launch per substep; default 9).  Each call is planned as the
+ * fewest odd-depth passes <= k, as even as possible.  Returns the previous
+ * value; k outside 1..15 only queries.  Bit-identical for every depth.     */
 int vk_set_stencil_depth(int32_t k);
 
 /* Fused-pass kernel variant: 0 = workgroup tile with an LDS neighbour
- * exchange, 1 = wave tile with DPP lane shifts (default); rows = output rows
- * per tile (8..4096; other values keep the current).  Returns the previous
- * variant.  Tuning only: results are bit-identical for every setting.     */
+ * exchange; 1 = wave tile with DPP lane shifts, stage q lagging 2q rows;
+ * 2 / 3 / 4 = wave tile, stage q lagging q rows (two live rows per stage),
+ * 3 / 6 / 9 rows prefetched (default 3).  rows = output rows per tile
+ * (8..4096; 0 = auto from the band height; other values keep the current).
+ * Returns the previous variant.  Tuning only: results are bit-identical for
+ * every setting.                                                           */
 int vk_set_stencil_kernel(int32_t variant, int32_t rows);
 
 /* dst[map_row[i]*ld + a] = fields[map_field[i]*field_stride + bin_lin[a]]. */

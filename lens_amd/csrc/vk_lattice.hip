@@ -513,7 +513,17 @@ __global__ __launch_bounds__(256) void k_diffuse_wl(const double *__restrict__ s
         diffuse_wl_body<K, PD, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
-static int g_stencil_rows = 64;
+static int g_stencil_rows = 64;   // output rows per wave tile; 0 = auto (chunk_rows below)
+
+// Rows per wave tile: g_stencil_rows, or (auto) the largest <= 64 that still
+// yields ~4 waves per SIMD on the 1024 SIMDs -- small row bands (multi-GPU
+// strong scaling) trade pipeline fill for occupancy.
+static int chunk_rows(int out_rows, int tiles_x, int nf) {
+    if (g_stencil_rows > 0) return g_stencil_rows;
+    const int64_t want_waves = 4096;
+    int r = (int)(((int64_t)out_rows * tiles_x * nf) / want_waves);
+    return std::max(16, std::min(64, r));
+}
 
 template <int K>
 static void launch_wt(hipStream_t st, const double *src, double *dst, const double *f0, int nf, int64_t fs,
@@ -521,8 +531,8 @@ static void launch_wt(hipStream_t st, const double *src, double *dst, const doub
                       const double *mm) {
     constexpr int KH = K + (K & 1);
     constexpr int W = WT_COLS - 2 * KH;
-    const int rch = g_stencil_rows;
     const int tiles_x = (ny + W - 1) / W;
+    const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
     const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
     if (f0)
@@ -541,8 +551,8 @@ static void launch_wl(hipStream_t st, const double *src, double *dst, const doub
                       const double *mm) {
     constexpr int KH = K + (K & 1);
     constexpr int W = WT_COLS - 2 * KH;
-    const int rch = g_stencil_rows;
     const int tiles_x = (ny + W - 1) / W;
+    const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
     const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
     if (f0)
@@ -579,7 +589,7 @@ static void launch_wt_k(int k, hipStream_t st, const double *src, double *dst, c
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
     if (variant >= 0 && variant <= 4) g_stencil_kernel = variant;
-    if (rows >= 8 && rows <= 4096) g_stencil_rows = rows;
+    if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
 }
 
@@ -707,70 +717,65 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
 // equal gets a zero delta).  Summary per plane: sum[2f] == sum[2f+1] iff the
 // owned rows hold one value (both = that value); otherwise (-inf, +inf).  The
 // summary min/max-reduces across ranks (distributed.make_uniform_allreduce).
-// A non-uniform plane is detected by the first blocks that run; every later
-// block reads the summary once and exits, so the common case costs a few
-// microseconds instead of a full read of the plane.
+// A fixed grid of VK_UNIFORM_BLOCKS blocks per plane strides over the plane
+// in 16-KiB chunks and stops at its first chunk holding a second value, so a
+// non-uniform plane costs one chunk per block (a few microseconds); every
+// block writes its own flag (no shared address is polled or stored to), and
+// a one-block pass folds the flags into the summary.
 // ---------------------------------------------------------------------------
 
-__global__ void k_uniform_init(const double *__restrict__ fields, int64_t field_stride, int64_t off,
-                               int n_fields, double *sum) {
-    const int f = threadIdx.x;
-    if (f < n_fields) {
-        const double v0 = fields[(int64_t)f * field_stride + off];
-        const bool nan = !(v0 == v0);   // NaN != NaN: a NaN plane is non-uniform
-        sum[2 * f] = nan ? -INFINITY : v0;
-        sum[2 * f + 1] = nan ? INFINITY : v0;
-    }
-}
-
 constexpr int UN_PER_THREAD = 8;
+constexpr int UN_CHUNK = 256 * UN_PER_THREAD;
 
 __global__ __launch_bounds__(256) void k_uniform_probe(const double *__restrict__ fields, int64_t field_stride,
-                                                       int64_t off, int64_t count, double *sum) {
+                                                       int64_t off, int64_t count, int32_t *__restrict__ found) {
     const int f = blockIdx.y;
-    double *vs = sum + 2 * f;
-    // one lane per block reads the summary (every lane polling one address
-    // serialises on a single L2 channel), the block shares it through LDS
-    __shared__ double s_v0;
-    __shared__ int s_done;
-    if (threadIdx.x == 0) {
-        const double lo = __hip_atomic_load(vs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double hi = __hip_atomic_load(vs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_v0 = lo;
-        s_done = !(lo == hi);                         // already non-uniform (or NaN)
-    }
-    __syncthreads();
-    if (s_done) return;
-    const double v0 = s_v0;
     const double *p = fields + (int64_t)f * field_stride + off;
-    const int64_t base = (int64_t)blockIdx.x * (256 * UN_PER_THREAD) + threadIdx.x;
-    bool diff = false;
+    const double v0 = p[0];
+    int hit = !(v0 == v0);                       // a NaN plane is non-uniform
+    for (int64_t c = blockIdx.x; !hit && c * UN_CHUNK < count; c += gridDim.x) {
+        const int64_t base = c * UN_CHUNK + threadIdx.x;
+        bool diff = false;
 #pragma unroll
-    for (int k = 0; k < UN_PER_THREAD; ++k) {
-        const int64_t i = base + (int64_t)k * 256;
-        if (i < count) diff |= !(p[i] == v0);
+        for (int k = 0; k < UN_PER_THREAD; ++k) {
+            const int64_t i = base + (int64_t)k * 256;
+            if (i < count) diff |= !(p[i] == v0);
+        }
+        hit = __syncthreads_or(diff);
     }
-    if (__syncthreads_or(diff) && threadIdx.x == 0) {
-        __hip_atomic_store(vs, -INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(vs + 1, INFINITY, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) found[(int64_t)f * gridDim.x + blockIdx.x] = hit;
+}
+
+__global__ __launch_bounds__(256) void k_uniform_finish(const double *__restrict__ fields, int64_t field_stride,
+                                                        int64_t off, const int32_t *__restrict__ found,
+                                                        int n_blocks, double *__restrict__ sum) {
+    const int f = blockIdx.x;
+    int hit = 0;
+    for (int b = threadIdx.x; b < n_blocks; b += 256) hit |= found[(int64_t)f * n_blocks + b];
+    hit = __syncthreads_or(hit);
+    if (threadIdx.x == 0) {
+        const double v0 = fields[(int64_t)f * field_stride + off];
+        sum[2 * f] = hit ? -INFINITY : v0;
+        sum[2 * f + 1] = hit ? INFINITY : v0;
     }
 }
 
 extern "C" int vk_field_uniform(const double *fields, int32_t n_fields, int64_t field_stride, int32_t ny,
-                                int32_t row_lo, int32_t row_hi, double *summary, vk_stream_t stream) {
-    if (!fields || !summary || n_fields < 0 || n_fields > 1024 || ny <= 0 || row_lo < 0 || row_hi <= row_lo ||
-        (int64_t)row_hi * ny > field_stride) {
+                                int32_t row_lo, int32_t row_hi, double *summary, int32_t *scratch,
+                                vk_stream_t stream) {
+    if (!fields || !summary || !scratch || n_fields < 0 || n_fields > 65535 || ny <= 0 || row_lo < 0 ||
+        row_hi <= row_lo || (int64_t)row_hi * ny > field_stride) {
         vk::set_error("vk_field_uniform: bad arguments");
         return VK_ERR_ARG;
     }
     if (n_fields == 0) return VK_OK;
     hipStream_t s = (hipStream_t)stream;
     const int64_t off = (int64_t)row_lo * ny;
-    hipLaunchKernelGGL(k_uniform_init, dim3(1), dim3(1024), 0, s, fields, field_stride, off, n_fields, summary);
     const int64_t count = (int64_t)(row_hi - row_lo) * ny;
-    const int64_t per_block = 256 * UN_PER_THREAD;
-    const unsigned blocks = (unsigned)((count + per_block - 1) / per_block);
+    const int blocks = (int)std::min<int64_t>(VK_UNIFORM_BLOCKS, (count + UN_CHUNK - 1) / UN_CHUNK);
     hipLaunchKernelGGL(k_uniform_probe, dim3(blocks, n_fields), dim3(256), 0, s, fields, field_stride, off, count,
+                       scratch);
+    hipLaunchKernelGGL(k_uniform_finish, dim3(n_fields), dim3(256), 0, s, fields, field_stride, off, scratch, blocks,
                        summary);
     return vk::launch_check("k_uniform_probe");
 }

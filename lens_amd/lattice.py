@@ -40,8 +40,9 @@ def stencil_depth(k: int = 0) -> int:
     return native._lib.vk_set_stencil_depth(int(k))
 
 
-def stencil_kernel(variant: int = -1, rows: int = 0) -> int:
-    """Select the fused-pass kernel (0 = workgroup/LDS, 1 = wave/DPP) and rows per tile."""
+def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
+    """Select the fused-pass kernel (0 = workgroup/LDS, 1 = wave/DPP lag-2, 2/3/4 = wave/DPP
+    lag-1 with 3/6/9 prefetched rows) and output rows per tile (0 = auto; -1 keeps)."""
     native.load()
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
 
@@ -83,6 +84,8 @@ class Lattice:
         self.work0 = torch.empty(shape, dtype=torch.float64, device=self.device)
         self.work1 = torch.empty(shape, dtype=torch.float64, device=self.device)
         self.uniform = torch.empty(2 * max(nf, 1), dtype=torch.float64, device=self.device)
+        self._uniform_scratch = torch.empty(max(nf, 1) * native.VK_UNIFORM_BLOCKS, dtype=torch.int32,
+                                            device=self.device)
         if initial is not None:
             for f, m in enumerate(self.molecules):
                 if m in initial:
@@ -122,7 +125,8 @@ class Lattice:
         holds one value; ``allreduce`` (multi-rank) makes it the global test."""
         native.check(native._lib.vk_field_uniform(
             native.ptr(self.fields), len(self.molecules), self.field_stride, self.ny, self.row_lo,
-            self.row_hi, native.ptr(self.uniform), native.stream_handle()), 'vk_field_uniform')
+            self.row_hi, native.ptr(self.uniform), native.ptr(self._uniform_scratch), native.stream_handle()),
+            'vk_field_uniform')
         if allreduce is not None:
             allreduce(self.uniform)
         return self.uniform

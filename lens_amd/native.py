@@ -37,6 +37,7 @@ VK_CELL_ROWS = 6
 VK_GROWTH_PROTEIN, VK_GROWTH_MASS = 0, 1
 VK_RNG_STREAM, VK_RNG_PHILOX = 0, 1
 VK_DIVIDE_SET, VK_DIVIDE_SPLIT, VK_DIVIDE_ZERO = 0, 1, 2
+VK_UNIFORM_BLOCKS = 512
 
 
 class NativeError(RuntimeError):
@@ -92,7 +93,7 @@ _SIGS = {
     'vk_step_euler': ([_vp, _i64, _i64, _f64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     'vk_step_dopri5': ([_vp, _i64, _i64, _f64, ctypes.POINTER(VkOdeOpts), _vp, _vp, _vp, _vp,
                         _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
-    'vk_field_uniform': ([_vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp], ctypes.c_int),
+    'vk_field_uniform': ([_vp, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp], ctypes.c_int),
     'vk_diffuse': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                     _i32, _i32, _i32, _f64, _vp, _vp], ctypes.c_int),
     'vk_set_stencil_depth': ([_i32], ctypes.c_int),
