@@ -63,6 +63,8 @@ def parse():
     p.add_argument('--stencil-depth', type=int, default=9)
     p.add_argument('--stencil-rows', type=int, default=None,
                    help='output rows per wave tile (default 64 on one GPU, 0 = auto on row bands)')
+    p.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
+                   help='nccl (= RCCL) for real runs; gloo stages through host memory (rehearsal only)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -186,12 +188,16 @@ def main():
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
-    dev = torch.device('cuda', local)
+    # one rank per GPU; a rehearsal with more ranks than GPUs (--dist-backend gloo) shares them
+    dev = torch.device('cuda', local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)       # RCCL over xGMI
+        else:
+            dist.init_process_group(args.dist_backend)
     from lens_amd.lattice import stencil_depth, stencil_kernel
     stencil_depth(args.stencil_depth)
     if args.stencil_rows is None:
@@ -239,6 +245,8 @@ def main():
                if lat is not None else 0.0)
     attempts = float(nsteps_acc.item())
     if dist is not None:
+        if args.dist_backend == 'gloo':
+            el, n_agents = el.cpu(), n_agents.cpu()
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(n_agents, op=dist.ReduceOp.SUM)
     elapsed = float(el.item())

@@ -29,6 +29,12 @@ def row_bands(nx: int, world: int) -> List[Tuple[int, int]]:
     return out
 
 
+def _host_staged(dev, group) -> bool:
+    """gloo moves host tensors: device buffers are staged through host memory
+    (rehearsal runs of the multi-rank path on one GPU; RCCL needs no staging)."""
+    return dev.type != 'cpu' and dist.get_backend(group) == 'gloo'
+
+
 def make_halo_exchange(lat, rank: int, world: int, group=None):
     """Callback for :meth:`Lattice.diffuse`: fill ``lat.halo`` rows above/below
     the owned band of ``src`` (a [n_fields, rows_local, ny] tensor) from the
@@ -39,7 +45,8 @@ def make_halo_exchange(lat, rank: int, world: int, group=None):
         raise ValueError('halo (%d) deeper than the band (%d rows)' % (h, owned))
     nf, ny = len(lat.molecules), lat.ny
     dev = lat.fields.device
-    bufs = {k: torch.empty((nf, h, ny), dtype=torch.float64, device=dev)
+    buf_dev = torch.device('cpu') if _host_staged(dev, group) else dev
+    bufs = {k: torch.empty((nf, h, ny), dtype=torch.float64, device=buf_dev)
             for k in ('send_up', 'send_dn', 'recv_up', 'recv_dn')}
 
     def exchange(src, cnt):
@@ -69,8 +76,11 @@ def make_uniform_allreduce(group=None):
     lo == hi afterwards iff every rank's band holds the same single value."""
 
     def allreduce(mm):
-        mm[0::2].neg_()
-        dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
-        mm[0::2].neg_()
+        t = mm.cpu() if _host_staged(mm.device, group) else mm
+        t[0::2].neg_()
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        t[0::2].neg_()
+        if t is not mm:
+            mm.copy_(t)
 
     return allreduce
