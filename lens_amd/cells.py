@@ -49,7 +49,7 @@ class CellModel:
     division_volume: float = 2.4           # fL, division_volume.py:13
     initial_mass: float = 1339.0           # fg
     protein_mw: float = 2.09e4             # g/mol, growth_protein.py:26
-    width: float = 1.0                     # um, derive_globals.py:60
+    width: float = 1                       # um, derive_globals.py:60 (an int there: emitted as 1)
     density: float = 1100.0                # g/L, derive_globals.py:93
     avogadro: float = N_A_LEGACY
     rng: str = 'stream'

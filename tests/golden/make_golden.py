@@ -236,7 +236,11 @@ def colony_metrics_fixture():
         out['k_' + aid] = np.array(keep)
         out['v_' + aid] = np.array([[series[j][k] for j in range(len(variables))] for k in keep])
     np.savez_compressed(os.path.join(HERE, 'colony_metrics_subset.npz'), **out)
-    print('wrote colony_metrics_subset.npz:', len(ids), 'agents')
+    # and the file itself (data: the emitter test rebuilds it byte for byte)
+    import gzip
+    with open(src, 'rb') as f, gzip.open(os.path.join(HERE, 'colony_metrics.csv.gz'), 'wb', 9) as g:
+        g.write(f.read())
+    print('wrote colony_metrics_subset.npz + colony_metrics.csv.gz:', len(ids), 'agents')
 
 
 if __name__ == '__main__':
