@@ -363,6 +363,48 @@ int vk_kremling_step(const vk_kremling_params *params, int64_t n_agents, int64_t
                      double *h_state, double *flux, int64_t *counts, int32_t *status,
                      int32_t *nsteps, vk_stream_t stream);
 
+/* ---------------------------------------------------------------------------
+ * ODE gene expression with boolean regulation:
+ * ODE_expression.next_update (vivarium/processes/ode_expression.py:265-303)
+ * with regulation rules (vivarium/library/regulation_logic.py) compiled by
+ * lens_amd/expression.py into postfix programs.
+ * ------------------------------------------------------------------------- */
+enum vk_expr_op {
+    VK_EXPR_CMP_GT = 0,   /* push conc[a] > thr[b]                       */
+    VK_EXPR_CMP_LT = 1,   /* push conc[a] < thr[b]                       */
+    VK_EXPR_PRESENT = 2,  /* push conc[a] > 0  (a lone numeric operand)  */
+    VK_EXPR_CONST = 3,    /* push a != 0                                 */
+    VK_EXPR_NOT = 4,
+    VK_EXPR_AND = 5,
+    VK_EXPR_OR = 6
+};
+
+/* All pointers are DEVICE arrays owned by the caller.  Programs are
+ * [op, a, b] int32 triples; transcript t's rule is code[prog_ptr[t] ..
+ * prog_ptr[t+1]) (empty = unregulated).                                     */
+typedef struct vk_expr_table {
+    int32_t n_tx, n_tl;
+    const int32_t *tx_row;        /* [n_tx] state row of each transcript      */
+    const double *tx_rate;        /* [n_tx] transcription rate                */
+    const double *tx_deg;         /* [n_tx] degradation rate (0 if absent)    */
+    const int32_t *tx_prog_ptr;   /* [n_tx+1]                                 */
+    const int32_t *code;          /* [3 * n_instr]                            */
+    const double *thr;            /* thresholds                               */
+    const int32_t *tl_row;        /* [n_tl] state row of each protein         */
+    const int32_t *tl_mrna_row;   /* [n_tl] its transcript's row              */
+    const double *tl_rate;        /* [n_tl] translation rate                  */
+    const double *tl_deg;         /* [n_tl] degradation rate                  */
+    double leak_p;                /* 1 - exp(-(-log(1 - rate)) * dt), host    */
+    double leak_magnitude;
+} vk_expr_table;
+
+/* update[j][ld] := the reference's {'internal': {...}} values, transcripts
+ * (j < n_tx) then proteins, all from the step-start conc; accumulate != 0
+ * then adds them into conc (the accumulate updater).  u[n_tx][ld] (nullable):
+ * uniforms for the leak draws of inhibited transcripts (NULL: no leak).      */
+int vk_expression_step(const vk_expr_table *t, int64_t n_agents, int64_t ld, double dt, double *conc,
+                       double *update, const double *u, int32_t accumulate, vk_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

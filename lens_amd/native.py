@@ -30,6 +30,7 @@ EXPORTS = (
     'vk_diffuse', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites', 'vk_cell_step', 'vk_divide_scratch_bytes', 'vk_divide_plan',
     'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations', 'vk_kremling_step',
+    'vk_expression_step',
 )
 
 VK_CELL_MASS, VK_CELL_VOLUME, VK_CELL_LENGTH, VK_CELL_SURFACE_AREA, VK_CELL_PROTEIN, VK_CELL_ANGLE = range(6)
@@ -110,6 +111,7 @@ _SIGS = {
     'vk_divide_gather': ([_i64, _vp, _vp, _vp, _i64, _vp, _i64, _i32, _i32, _i32, _vp], ctypes.c_int),
     'vk_divide_lineage': ([_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
     'vk_divide_locations': ([_i64, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp], ctypes.c_int),
+    'vk_expression_step': ([_vp, _i64, _i64, _f64, _vp, _vp, _vp, _i32, _vp], ctypes.c_int),
     'vk_kremling_step': ([ctypes.POINTER(VkKremlingParams), _i64, _i64, _f64, _f64, _i32, _f64, _f64, _i32,
                           _vp, _vp, _f64, _vp, _vp, _vp, _vp, _vp, _vp], ctypes.c_int),
 }
