@@ -369,7 +369,7 @@ __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ s
 
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
 template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U>
-__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD],
+__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                         const double *__restrict__ s, double *__restrict__ d,
                                         const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
@@ -383,7 +383,10 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     const int r_out = i - K;
     const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
     double2 base = make_double2(0.0, 0.0);
-    if (FINAL && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
+    if (FINAL) {   // base row r_out arrived 3 iterations ago; fetch row r_out+3 (clamped into the chunk)
+        base = gp[R];
+        if (L.wA || L.wB) gp[R] = wt_load<EDGE>(g, (int64_t)min(max(r_out + 3, c0), c1 - 1) * ny, L);
+    }
 #pragma unroll
     for (int q = 0; q < K; ++q) {
         // stage q is useful for rows [c0-(K-1-q), c1+(K-1-q)), i.e. i in [c0-K+2+2q, c1+K)
@@ -420,32 +423,32 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
 
 template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
-                                         double2 (&pf)[PD], const double *__restrict__ s, double *__restrict__ d,
+                                         double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *__restrict__ d,
                                          const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
-    wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect,
+    wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect,
                                         bot_reflect, coef);
     if constexpr (sizeof...(Us) > 0)
-        wl_group<K, PD, EDGE, FINAL, STEADY, Us...>(S0, S1, S2, pf, s, d, g, L, i + 1, c0, c1, in_lo, in_hi,
+        wl_group<K, PD, EDGE, FINAL, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo, in_hi,
                                                 top_reflect, bot_reflect, coef);
 }
 
 template <int K, int PD, bool EDGE, bool FINAL, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
-                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD],
+                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                                 const double *__restrict__ s, double *__restrict__ d,
                                                 const double *__restrict__ g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef) {
     const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
     const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
-#define WL_ARGS S0, S1, S2, pf, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef
+#define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef
     int i = i0;
     for (; i + PD <= i1 && i < s_lo; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);   // fill
     for (; i + PD - 1 <= s_hi; i += PD) wl_group<K, PD, EDGE, FINAL, true, Us...>(WL_ARGS);          // steady
     for (; i + PD <= i1; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);               // drain
     // tail: fewer than PD iterations, phases 0.. in order
-    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, false, Us>(S0, S1, S2, pf, s, d, g, L, i + Us, c0, c1, in_lo,
+    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1, in_lo,
                                                         in_hi, top_reflect, bot_reflect, coef)
                   : void()), ...);
 #undef WL_ARGS
@@ -456,7 +459,7 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
                                                 const double *__restrict__ g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef) {
-    double2 S0[K], S1[K], S2[K], pf[PD];
+    double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
 #pragma unroll
     for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
     const int64_t ny = L.ny;
@@ -466,7 +469,11 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
     S1[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 1, in_lo), in_hi - 1) * ny, L);
 #pragma unroll
     for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
-    diffuse_wl_loop<K, PD, EDGE, FINAL>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, s, d, g, L, c0, c1,
+#pragma unroll
+    for (int u = 0; u < 3; ++u)   // FINAL: base rows of the first 3 output rows (i0 - K + u)
+        gp[u] = FINAL && (L.wA || L.wB) ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
+                                        : make_double2(0.0, 0.0);
+    diffuse_wl_loop<K, PD, EDGE, FINAL>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L, c0, c1,
                                     in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
@@ -687,7 +694,10 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform);
         } else if (g_stencil_kernel >= 2) {
-            auto launch = g_stencil_kernel == 2 ? launch_wl_k<3> : (g_stencil_kernel == 3 ? launch_wl_k<6> : launch_wl_k<9>);
+            // the final pass also streams the base plane (3 rows ahead): it keeps the
+            // shallow row prefetch so that it still fits 3 waves per SIMD
+            auto launch = (g_stencil_kernel == 2 || f0) ? launch_wl_k<3>
+                                                        : (g_stencil_kernel == 3 ? launch_wl_k<6> : launch_wl_k<9>);
             launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
                    coeff_dt, uniform);
         } else if (g_stencil_kernel == 1) {
