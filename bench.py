@@ -45,6 +45,19 @@ WORKLOADS = {
 }
 
 
+def stencil_kernel_name(variant, depth):
+    """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
+    if variant == 0:
+        return 'k_diffuse_tb<%d>' % depth
+    if variant == 1:
+        return 'k_diffuse_wt<%d, false>' % depth
+    if variant == 5:
+        return 'k_diffuse_wl4<%d, 6, false>' % depth
+    if variant in (6, 7):
+        return '%s::k_diffuse_wl<%d, 6, false>' % ('vk_nt' if variant == 6 else 'vk_ntl', depth)
+    return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 * (variant - 1))
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
@@ -58,8 +71,9 @@ def parse():
     p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=3,
-                   help='0 workgroup/LDS, 1 wave/DPP lag-2, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows')
+    p.add_argument('--stencil-kernel', type=int, default=6,
+                   help='0 workgroup/LDS, 1 wave/DPP lag-2, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows, '
+                        '5 = 3 capped at 4 waves/SIMD, 6/7 = 3 with streaming stores / loads+stores')
     p.add_argument('--stencil-depth', type=int, default=9)
     p.add_argument('--stencil-rows', type=int, default=None,
                    help='output rows per wave tile (default 64 on one GPU, 0 = auto on row bands)')
@@ -282,9 +296,7 @@ def main():
                 if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant')) == (
                         depth, args.stencil_rows, cells, args.stencil_kernel):
                     traffic = rec.get('hbm_bytes_per_launch')
-            kname = ('k_diffuse_wl<%d, %d, false>' % (depth, 3 * (args.stencil_kernel - 1))
-                     if args.stencil_kernel >= 2 else
-                     'k_diffuse_wt<%d, false>' % depth if args.stencil_kernel == 1 else 'k_diffuse_tb<%d>' % depth)
+            kname = stencil_kernel_name(args.stencil_kernel, depth)
             roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
                         'traffic': traffic, 'bytes_per_launch': bytes_per_launch,

@@ -192,7 +192,9 @@ int vk_set_stencil_depth(int32_t k);
 /* Fused-pass kernel variant: 0 = workgroup tile with an LDS neighbour
  * exchange; 1 = wave tile with DPP lane shifts, stage q lagging 2q rows;
  * 2 / 3 / 4 = wave tile, stage q lagging q rows (two live rows per stage),
- * 3 / 6 / 9 rows prefetched (default 3).  rows = output rows per tile
+ * 3 / 6 / 9 rows prefetched; 5 = variant 3 capped at 4 waves per SIMD;
+ * 6 = variant 3 with streaming (non-temporal) stores (default); 7 = variant
+ * 6 with streaming loads too.  rows = output rows per tile
  * (8..4096; 0 = auto from the band height; other values keep the current).
  * Returns the previous variant.  Tuning only: results are bit-identical for
  * every setting.                                                           */

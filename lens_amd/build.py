@@ -8,25 +8,27 @@ from __future__ import annotations
 import glob
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SRC = sorted(glob.glob(os.path.join(HERE, 'csrc', '*.hip')))
-HDRS = sorted(glob.glob(os.path.join(HERE, 'csrc', '*.h'))) + [os.path.join(REPO, 'include', 'vk_kinetics.h')]
+HDRS = sorted(glob.glob(os.path.join(HERE, 'csrc', '*.h')) + glob.glob(os.path.join(HERE, 'csrc', '*.inc'))) + [os.path.join(REPO, 'include', 'vk_kinetics.h')]
 OUT = os.path.join(HERE, 'lib', 'libvk_kinetics.so')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ARCH = 'gfx950'
 
-FLAGS = [
-    '--offload-arch=' + ARCH, '-O3', '-std=c++17', '-fPIC', '-shared',
+COMPILE = [
+    '--offload-arch=' + ARCH, '-O3', '-std=c++17', '-fPIC',
     # the exact kernels reproduce the reference's rounding sequence; FMAs are
     # written explicitly where a kernel wants them
     '-ffp-contract=off',
     '-Wall', '-Wno-unused-function',
     '-I' + os.path.join(REPO, 'include'), '-I' + os.path.join(HERE, 'csrc'),
-    '-Wl,-rpath,/opt/rocm/lib', '-lhiprtc',
 ]
+LINK = ['--offload-arch=' + ARCH, '-shared', '-fPIC', '-Wl,--no-undefined', '-Wl,-rpath,/opt/rocm/lib', '-lhiprtc']
+OBJ_DIR = os.path.join(HERE, 'lib', 'obj')
 
 
 def _stale(out, deps):
@@ -39,7 +41,23 @@ def _stale(out, deps):
 def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     if force or _stale(OUT, SRC + HDRS + [__file__]):
-        cmd = [HIPCC] + FLAGS + SRC + ['-o', OUT + '.tmp']
+        # one hipcc per translation unit, in parallel (the stencil launchers are
+        # split over several units so their template instantiations spread out)
+        os.makedirs(OBJ_DIR, exist_ok=True)
+        objs = [os.path.join(OBJ_DIR, os.path.basename(src)[:-4] + '.o') for src in SRC]
+        todo = [(src, obj) for src, obj in zip(SRC, objs) if force or _stale(obj, [src] + HDRS + [__file__])]
+        jobs = max(1, min(len(todo), int(os.environ.get('MAX_JOBS', '0')) or (os.cpu_count() or 1)))
+
+        def compile_one(pair):
+            cmd = [HIPCC] + COMPILE + ['-c', pair[0], '-o', pair[1] + '.tmp']
+            if verbose:
+                print('[lens_amd.build]', ' '.join(cmd), flush=True)
+            subprocess.run(cmd, check=True)
+            os.replace(pair[1] + '.tmp', pair[1])
+
+        with ThreadPoolExecutor(jobs) as ex:
+            list(ex.map(compile_one, todo))
+        cmd = [HIPCC] + LINK + objs + ['-o', OUT + '.tmp']
         if verbose:
             print('[lens_amd.build]', ' '.join(cmd), flush=True)
         subprocess.run(cmd, check=True)

@@ -1,0 +1,539 @@
+// Fused-pass stencil kernels (temporal blocking), shared by the stencil
+// translation units.  Each vk_stencil_*.hip instantiates one family of
+// launchers, so the (many) template instantiations compile in parallel;
+// vk_lattice.hip (vk_diffuse) calls them through vk_stencil_launch.h.
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <utility>
+
+#include "vk_internal.h"
+#include "vk_stencil_launch.h"
+
+// ---------------------------------------------------------------------------
+// Temporally blocked stencil: K substeps per pass over HBM.
+//
+// A workgroup owns a tile of TB_BX columns (TB_BX-2K output columns + K halo
+// columns per side) and a chunk of output rows; it streams its input rows
+// top to bottom once.  Substep s (0-based) is a pipeline stage holding a
+// three-row window (up, centre, newest) per column in VGPRs; at iteration i
+// stage s produces row i-2s-1, and its output becomes stage s+1's newest
+// row in iteration i+1, so all K stages of an iteration are independent and
+// share ONE LDS exchange of centre values (left/right neighbours) and ONE
+// barrier (LDS double-buffered by iteration parity).  HBM traffic per pass:
+// one read of (chunk+2K) rows and one write of chunk rows, instead of K reads
+// and K writes.  The arithmetic per cell and substep is the reference's
+// ((up + left) + (-4*c)) + right) + down, c + coef*lap -- fma(-4, c, s) is
+// bit-identical to s + (-4*c) because -4*c is exact.
+// ---------------------------------------------------------------------------
+
+constexpr int TB_BX = 256;
+
+// One pipeline iteration with static register roles U (loop unrolled by 3, so
+// the three-row windows rotate by renaming instead of v_mov).  For stage q:
+// up = X[U], centre = X[U+1], newest = X[U+2] (mod 3); stage q-1's output is
+// stage q's newest next iteration and lands in X[U] once stage q consumed it.
+template <int K, bool EDGE, int U>
+__device__ __forceinline__ void tb_iter(double (&xch)[2][K][TB_BX], double (&X0)[K], double (&X1)[K],
+                                        double (&X2)[K], double (&pf)[3], const double *__restrict__ s,
+                                        double *__restrict__ d, const double *__restrict__ g, int ny, int i,
+                                        int c0, int c1, int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                        int c, int cc, bool writer, int tl, int tr, bool left_edge,
+                                        bool right_edge, double coef) {
+    double(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
+    double(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
+    double(&NW)[K] = U == 0 ? X2 : (U == 1 ? X0 : X1);
+    const int tid = threadIdx.x;
+    NW[0] = pf[U];                                                    // row i, loaded 3 iterations ago
+    pf[U] = s[(int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny + cc];  // prefetch row i+3
+    const int r_out = i - 2 * K + 1;
+    const bool do_write = writer && r_out >= c0 && r_out < c1;
+    double base = 0.0;
+    if (g && do_write) base = g[(int64_t)r_out * ny + c];
+    const int p = i & 1;
+#pragma unroll
+    for (int q = 0; q < K; ++q) xch[p][q][tid] = CN[q];
+    __syncthreads();
+#pragma unroll
+    for (int q = K - 1; q >= 0; --q) {
+        const int r = i - 2 * q - 1;
+        const double cen = CN[q];
+        const double up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double dn = (EDGE && r == bot_reflect) ? cen : NW[q];
+        const double lv = xch[p][q][tl], rv = xch[p][q][tr];
+        const double lf = left_edge ? cen : lv;
+        const double rt = right_edge ? cen : rv;
+        const double lap = ((fma(-4.0, cen, up + lf)) + rt) + dn;
+        const double v = cen + coef * lap;
+        if (q + 1 < K) {
+            UP[q + 1] = v;
+        } else if (do_write) {
+            d[(int64_t)r_out * ny + c] = g ? base + (v - base) : v;
+        }
+    }
+}
+
+// EDGE = the tile touches a reflecting boundary (global edge rows/columns);
+// interior tiles (the vast majority) carry no boundary selects at all.
+template <int K, bool EDGE>
+__device__ __forceinline__ void diffuse_tb_body(double (&xch)[2][K][TB_BX], const double *__restrict__ s,
+                                                double *__restrict__ d, const double *__restrict__ g, int ny,
+                                                int c0, int c1, int in_lo, int in_hi, int top_reflect,
+                                                int bot_reflect, int x0, double coef) {
+    const int tid = threadIdx.x;
+    const int c = x0 - K + tid;
+    const int cc = min(max(c, 0), ny - 1);
+    const bool left_edge = EDGE && (c == 0), right_edge = EDGE && (c == ny - 1);
+    const bool writer = tid >= K && tid < TB_BX - K && c < ny;
+    const int tl = max(tid - 1, 0), tr = min(tid + 1, TB_BX - 1);
+
+    double X0[K], X1[K], X2[K], pf[3];
+#pragma unroll
+    for (int q = 0; q < K; ++q) X0[q] = X1[q] = X2[q] = 0.0;
+    const int i0 = c0 - K, i1 = c1 + 2 * K - 1;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) pf[u] = s[(int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny + cc];
+#define TB_ARGS xch, X0, X1, X2, pf, s, d, g, ny
+#define TB_REST c0, c1, in_lo, in_hi, top_reflect, bot_reflect, c, cc, writer, tl, tr, left_edge, right_edge, coef
+    int i = i0;
+    for (; i + 3 <= i1; i += 3) {
+        tb_iter<K, EDGE, 0>(TB_ARGS, i, TB_REST);
+        tb_iter<K, EDGE, 1>(TB_ARGS, i + 1, TB_REST);
+        tb_iter<K, EDGE, 2>(TB_ARGS, i + 2, TB_REST);
+    }
+    if (i < i1) tb_iter<K, EDGE, 0>(TB_ARGS, i, TB_REST);
+    if (i + 1 < i1) tb_iter<K, EDGE, 1>(TB_ARGS, i + 1, TB_REST);
+#undef TB_ARGS
+#undef TB_REST
+}
+
+template <int K>
+__global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__ src, double *__restrict__ dst,
+                                                      const double *__restrict__ f0, int64_t field_stride, int ny,
+                                                      int out_lo, int out_hi, int in_lo, int in_hi,
+                                                      int top_reflect, int bot_reflect, int rows_per_chunk,
+                                                      double coef, const double *__restrict__ uniform) {
+    const int f = blockIdx.z;
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform plane: zero delta
+    const int c0 = out_lo + blockIdx.y * rows_per_chunk;
+    if (c0 >= out_hi) return;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = blockIdx.x * (TB_BX - 2 * K);
+    __shared__ double xch[2][K][TB_BX];
+    const double *s = src + (int64_t)f * field_stride;
+    double *d = dst + (int64_t)f * field_stride;
+    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    // rows this block touches: [c0-K-1, c1+2K); columns [x0-K-1, x0-K+TB_BX]
+    const bool edge = (x0 - K - 1 <= 0) || (x0 - K + TB_BX >= ny - 1) ||
+                      (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
+                      (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
+    if (edge)
+        diffuse_tb_body<K, true>(xch, s, d, g, ny, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, x0, coef);
+    else
+        diffuse_tb_body<K, false>(xch, s, d, g, ny, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, x0, coef);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-tile variant: one wavefront = one independent tile of 128 columns (two
+// adjacent columns per lane), so there is no LDS and no barrier at all.  The
+// left/right neighbours come from the lane itself (A<->B) and from the
+// adjacent lanes through DPP wave shifts (v_mov_b32_dpp wave_shr:1 /
+// wave_shl:1); the tile's outer KH columns per side are the halo that the K
+// fused substeps eat into.  Loads/stores are 16 B per lane.
+// ---------------------------------------------------------------------------
+
+constexpr int WT_COLS = 128;
+
+// bound_ctrl = true: the lane shifted in from outside the wave reads 0 (that
+// lane is tile halo), so no "old" operand has to be materialised.
+__device__ __forceinline__ double dpp_from_lane_below(double v) {  // lane l <- lane l-1
+    int2 x = __builtin_bit_cast(int2, v);
+    int2 y;
+    y.x = __builtin_amdgcn_mov_dpp(x.x, 0x138, 0xf, 0xf, true);
+    y.y = __builtin_amdgcn_mov_dpp(x.y, 0x138, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, y);
+}
+
+__device__ __forceinline__ double dpp_from_lane_above(double v) {  // lane l <- lane l+1
+    int2 x = __builtin_bit_cast(int2, v);
+    int2 y;
+    y.x = __builtin_amdgcn_mov_dpp(x.x, 0x130, 0xf, 0xf, true);
+    y.y = __builtin_amdgcn_mov_dpp(x.y, 0x130, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, y);
+}
+
+// Full-tile store of one lane's two columns.  VK_WL_NT_STORE (set by a
+// translation unit before including this header) makes it a streaming store:
+// the written plane is read again only by the next pass.
+__device__ __forceinline__ void wl_store(double *o, double2 v) {
+#ifdef VK_WL_NT_STORE
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    d2v w = {v.x, v.y};
+    __builtin_nontemporal_store(w, reinterpret_cast<d2v *>(o));
+#else
+    *reinterpret_cast<double2 *>(o) = v;
+#endif
+}
+
+struct WtLane {
+    int cA;              // this lane's first column (cB = cA + 1)
+    int ny;
+    bool wA, wB;         // writes its column A / B
+    bool lA, rA, lB, rB; // reflect flags (EDGE tiles only)
+};
+
+template <bool EDGE>
+__device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t row_off, const WtLane &L) {
+    if (!EDGE) {
+#ifdef VK_WL_NT_LOAD
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const d2v w = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p + row_off + L.cA));
+        return make_double2(w.x, w.y);
+#else
+        return *reinterpret_cast<const double2 *>(p + row_off + L.cA);
+#endif
+    }
+    const int a = min(max(L.cA, 0), L.ny - 1), b = min(max(L.cA + 1, 0), L.ny - 1);
+    return make_double2(p[row_off + a], p[row_off + b]);
+}
+
+// STEADY: every stage is inside its useful row range (no fill/drain test),
+// so the K stages are straight-line code the scheduler can interleave.
+template <int K, bool EDGE, bool FINAL, bool STEADY, int U>
+__device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], double2 (&X2)[K], double2 (&pf)[3],
+                                        const double *__restrict__ s, double *__restrict__ d,
+                                        const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    double2(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
+    double2(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
+    double2(&NW)[K] = U == 0 ? X2 : (U == 1 ? X0 : X1);
+    const int64_t ny = L.ny;
+    NW[0] = pf[U];                                                                   // row i
+    pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny, L);  // prefetch row i+3
+    const int r_out = i - 2 * K + 1;
+    const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
+    double2 base = make_double2(0.0, 0.0);
+    if (FINAL && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
+#pragma unroll
+    for (int q = K - 1; q >= 0; --q) {
+        // stage q only matters for output rows [c0-(K-1-q), c1+(K-1-q)):
+        // skip the pipeline fill/drain iterations (wave-uniform branch)
+        if (!STEADY && (i < c0 - K + 3 * q + 2 || i > c1 + K - 1 + q)) continue;
+        const int r = i - 2 * q - 1;
+        const double2 cen = CN[q];
+        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double2 dn = (EDGE && r == bot_reflect) ? cen : NW[q];
+        double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
+        double rightA = cen.y, leftB = cen.x;
+        if (EDGE) {
+            leftA = L.lA ? cen.x : leftA;
+            rightA = L.rA ? cen.x : rightA;
+            leftB = L.lB ? cen.y : leftB;
+            rightB = L.rB ? cen.y : rightB;
+        }
+        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
+        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
+        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
+        if (q + 1 < K) {
+            UP[q + 1] = v;
+        } else if (row_ok) {
+            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            double *o = d + (int64_t)r_out * ny + L.cA;
+            if (!EDGE) {
+                if (L.wA) *reinterpret_cast<double2 *>(o) = v;
+            } else {
+                if (L.wA) o[0] = v.x;
+                if (L.wB) o[1] = v.y;
+            }
+        }
+    }
+}
+
+template <int K, bool EDGE, bool FINAL>
+__device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, double *__restrict__ d,
+                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                                double coef) {
+    double2 X0[K], X1[K], X2[K], pf[3];
+#pragma unroll
+    for (int q = 0; q < K; ++q) X0[q] = X1[q] = X2[q] = make_double2(0.0, 0.0);
+    const int i0 = c0 - K, i1 = c1 + 2 * K - 1;
+    const int64_t ny = L.ny;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
+    // iterations [s_lo, s_hi] have every stage active (fill ends, drain not begun)
+    const int s_lo = c0 + 2 * K - 1, s_hi = c1 + K - 1;
+#define WT_RUN(ST, U, I) wt_iter<K, EDGE, FINAL, ST, U>(X0, X1, X2, pf, s, d, g, L, I, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef)
+    int i = i0;
+    for (; i + 3 <= i1 && i < s_lo; i += 3) {   // fill
+        WT_RUN(false, 0, i); WT_RUN(false, 1, i + 1); WT_RUN(false, 2, i + 2);
+    }
+    for (; i + 2 <= s_hi; i += 3) {              // steady state: branch-free stages
+        WT_RUN(true, 0, i); WT_RUN(true, 1, i + 1); WT_RUN(true, 2, i + 2);
+    }
+    for (; i + 3 <= i1; i += 3) {                // drain
+        WT_RUN(false, 0, i); WT_RUN(false, 1, i + 1); WT_RUN(false, 2, i + 2);
+    }
+    if (i < i1) WT_RUN(false, 0, i);
+    if (i + 1 < i1) WT_RUN(false, 1, i + 1);
+#undef WT_RUN
+}
+
+template <int K, bool FINAL>
+__global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ src, double *__restrict__ dst,
+                                                    const double *__restrict__ f0, int64_t field_stride, int ny,
+                                                    int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
+                                                    int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
+                                                    int n_fields, double coef, const double *__restrict__ uniform) {
+    constexpr int KH = K + (K & 1);           // even halo keeps 16-B alignment
+    constexpr int W = WT_COLS - 2 * KH;       // output columns per tile
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int lane = threadIdx.x & 63;
+    if (wave >= tiles_x * chunks_y * n_fields) return;
+    const int tx = wave % tiles_x;
+    const int ty = (wave / tiles_x) % chunks_y;
+    const int f = wave / (tiles_x * chunks_y);
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform plane: zero delta
+    const int c0 = out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = tx * W;                    // first output column
+    WtLane L;
+    L.ny = ny;
+    L.cA = x0 - KH + 2 * lane;
+    const int cB = L.cA + 1;
+    L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
+    L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
+    L.lA = L.cA == 0;
+    L.rA = L.cA == ny - 1;
+    L.lB = cB == 0;
+    L.rB = cB == ny - 1;
+    const double *s = src + (int64_t)f * field_stride;
+    double *d = dst + (int64_t)f * field_stride;
+    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    // reflecting boundaries or ragged columns inside the tile -> EDGE body
+    const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
+                      (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
+                      (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
+    if (edge)
+        diffuse_wt_body<K, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    else
+        diffuse_wt_body<K, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+// ---------------------------------------------------------------------------
+// Wave-tile, lag-1 pipeline (variant 2).  Same tile / DPP scheme as
+// k_diffuse_wt, but stage q consumes stage q-1's output of the SAME iteration
+// (stage q computes row i-1-q at iteration i).  At the start of an iteration
+// each stage holds only two live rows (up, centre) instead of three, so the
+// register footprint drops from ~3K to ~2K row-pairs and more waves fit per
+// SIMD; the price is a dependency chain through the stages of one iteration,
+// which the unrolled body and the extra waves overlap.  Slot roles rotate with
+// the iteration phase U (period 3): up = S[U], centre = S[U+1], fresh = S[U+2].
+// ---------------------------------------------------------------------------
+
+// PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
+template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U>
+__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
+                                        const double *__restrict__ s, double *__restrict__ d,
+                                        const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    constexpr int R = U % 3;
+    double2(&UP)[K] = R == 0 ? S0 : (R == 1 ? S1 : S2);
+    double2(&CN)[K] = R == 0 ? S1 : (R == 1 ? S2 : S0);
+    double2(&FR)[K] = R == 0 ? S2 : (R == 1 ? S0 : S1);
+    const int64_t ny = L.ny;
+    FR[0] = pf[U];                                                                          // row i
+    pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L);     // row i+PD
+    const int r_out = i - K;
+    const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
+    double2 base = make_double2(0.0, 0.0);
+    if (FINAL) {   // base row r_out arrived 3 iterations ago; fetch row r_out+3 (clamped into the chunk)
+        base = gp[R];
+        if (L.wA || L.wB) gp[R] = wt_load<EDGE>(g, (int64_t)min(max(r_out + 3, c0), c1 - 1) * ny, L);
+    }
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        // stage q is useful for rows [c0-(K-1-q), c1+(K-1-q)), i.e. i in [c0-K+2+2q, c1+K)
+        if (!STEADY && (i < c0 - K + 2 + 2 * q || i >= c1 + K)) continue;
+        const int r = i - 1 - q;
+        const double2 cen = CN[q];
+        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double2 dn = (EDGE && r == bot_reflect) ? cen : FR[q];
+        double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
+        double rightA = cen.y, leftB = cen.x;
+        if (EDGE) {
+            leftA = L.lA ? cen.x : leftA;
+            rightA = L.rA ? cen.x : rightA;
+            leftB = L.lB ? cen.y : leftB;
+            rightB = L.rB ? cen.y : rightB;
+        }
+        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
+        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
+        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
+        if (q + 1 < K) {
+            FR[q + 1] = v;
+        } else if (row_ok) {
+            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            double *o = d + (int64_t)r_out * ny + L.cA;
+            if (!EDGE) {
+                if (L.wA) wl_store(o, v);
+            } else {
+                if (L.wA) o[0] = v.x;
+                if (L.wB) o[1] = v.y;
+            }
+        }
+    }
+}
+
+template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U0, int... Us>
+__device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
+                                         double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *__restrict__ d,
+                                         const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect,
+                                        bot_reflect, coef);
+    if constexpr (sizeof...(Us) > 0)
+        wl_group<K, PD, EDGE, FINAL, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo, in_hi,
+                                                top_reflect, bot_reflect, coef);
+}
+
+template <int K, int PD, bool EDGE, bool FINAL, int... Us>
+__device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
+                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
+                                                const double *__restrict__ s, double *__restrict__ d,
+                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                                double coef) {
+    const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
+    const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
+#define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef
+    int i = i0;
+    for (; i + PD <= i1 && i < s_lo; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);   // fill
+    for (; i + PD - 1 <= s_hi; i += PD) wl_group<K, PD, EDGE, FINAL, true, Us...>(WL_ARGS);          // steady
+    for (; i + PD <= i1; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);               // drain
+    // tail: fewer than PD iterations, phases 0.. in order
+    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1, in_lo,
+                                                        in_hi, top_reflect, bot_reflect, coef)
+                  : void()), ...);
+#undef WL_ARGS
+}
+
+template <int K, int PD, bool EDGE, bool FINAL>
+__device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *__restrict__ d,
+                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
+                                                double coef) {
+    double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
+#pragma unroll
+    for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
+    const int64_t ny = L.ny;
+    const int i0 = c0 - K + 2;
+    // stage 0's window before the first iteration: up = row i0-2, centre = row i0-1
+    S0[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 2, in_lo), in_hi - 1) * ny, L);
+    S1[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 1, in_lo), in_hi - 1) * ny, L);
+#pragma unroll
+    for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
+#pragma unroll
+    for (int u = 0; u < 3; ++u)   // FINAL: base rows of the first 3 output rows (i0 - K + u)
+        gp[u] = FINAL && (L.wA || L.wB) ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
+                                        : make_double2(0.0, 0.0);
+    diffuse_wl_loop<K, PD, EDGE, FINAL>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L, c0, c1,
+                                    in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+template <int K, int PD, bool FINAL>
+__device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *__restrict__ dst,
+                                                const double *__restrict__ f0, int64_t field_stride, int ny,
+                                                int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
+                                                int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
+                                                int n_fields, double coef, const double *__restrict__ uniform) {
+    constexpr int KH = K + (K & 1);
+    constexpr int W = WT_COLS - 2 * KH;
+    // (An XCD-contiguous tile order -- each XCD's L2 serving its tiles' shared
+    // halo columns -- measured 4 % slower on 4096^2: the halo re-reads already
+    // hit the die-level Infinity Cache, so plain round-robin order is kept.)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int lane = threadIdx.x & 63;
+    if (wave >= tiles_x * chunks_y * n_fields) return;
+    const int tx = wave % tiles_x;
+    const int ty = (wave / tiles_x) % chunks_y;
+    const int f = wave / (tiles_x * chunks_y);
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;
+    const int c0 = out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = tx * W;
+    WtLane L;
+    L.ny = ny;
+    L.cA = x0 - KH + 2 * lane;
+    const int cB = L.cA + 1;
+    L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
+    L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
+    L.lA = L.cA == 0;
+    L.rA = L.cA == ny - 1;
+    L.lB = cB == 0;
+    L.rB = cB == ny - 1;
+    const double *s = src + (int64_t)f * field_stride;
+    double *d = dst + (int64_t)f * field_stride;
+    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
+                      (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
+                      (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
+    if (edge)
+        diffuse_wl_body<K, PD, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+    else
+        diffuse_wl_body<K, PD, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+}
+
+#define VK_WL_PARAMS                                                                                           \
+    const double *__restrict__ src, double *__restrict__ dst, const double *__restrict__ f0, int64_t field_stride, \
+        int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect, int bot_reflect, int rows_per_chunk, \
+        int tiles_x, int chunks_y, int n_fields, double coef, const double *__restrict__ uniform
+#define VK_WL_ARGS                                                                                             \
+    src, dst, f0, field_stride, ny, out_lo, out_hi, in_lo, in_hi, top_reflect, bot_reflect, rows_per_chunk,      \
+        tiles_x, chunks_y, n_fields, coef, uniform
+
+template <int K, int PD, bool FINAL>
+__global__ __launch_bounds__(256) void k_diffuse_wl(VK_WL_PARAMS) {
+    diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
+}
+
+// Variant 5: the same tile with the register budget capped at 4 waves per SIMD
+// (128 VGPRs): the scheduler keeps fewer rows in flight per wave, and the
+// extra wave per SIMD overlaps one wave's row loads with another's stages.
+template <int K, int PD, bool FINAL>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_diffuse_wl4(VK_WL_PARAMS) {
+    diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
+}
+
+
+// Rows per wave tile: g_stencil_rows, or (auto) the largest <= 64 that still
+// yields ~4 waves per SIMD on the 1024 SIMDs -- small row bands (multi-GPU
+// strong scaling) trade pipeline fill for occupancy.
+static int chunk_rows(int out_rows, int tiles_x, int nf) {
+    if (::g_stencil_rows > 0) return ::g_stencil_rows;
+    const int64_t want_waves = 4096;
+    int r = (int)(((int64_t)out_rows * tiles_x * nf) / want_waves);
+    return std::max(16, std::min(64, r));
+}
+
+template <int K>
+static void launch_wt(hipStream_t st, const double *src, double *dst, const double *f0, int nf, int64_t fs,
+                      int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot, double coef,
+                      const double *mm) {
+    constexpr int KH = K + (K & 1);
+    constexpr int W = WT_COLS - 2 * KH;
+    const int tiles_x = (ny + W - 1) / W;
+    const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
+    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
+    const int waves = tiles_x * chunks_y * nf;
+    if (f0)
+        hipLaunchKernelGGL((k_diffuse_wt<K, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny,
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+    else
+        hipLaunchKernelGGL((k_diffuse_wt<K, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny,
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
+}
+

@@ -15,7 +15,7 @@ tail -1 gpurun_out/smoke.log
 timeout -k 10 600 python bench.py --steps $STEPS --warmup 3 > gpurun_out/bench_$TAG.log 2>&1 || { tail -20 gpurun_out/bench_$TAG.log; exit 4; }
 tail -1 gpurun_out/bench_$TAG.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { tail -30 gpurun_out/prof_$TAG.log; exit 5; }
-export VARIANT=${VARIANT:-3} DEPTH=${DEPTH:-9} ROWS=${ROWS:-64} REPS=2
+export VARIANT=${VARIANT:-6} DEPTH=${DEPTH:-9} ROWS=${ROWS:-64} REPS=2
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_${TAG}_$c -o run -- python3 scripts/stencil_once.py > gpurun_out/pmc_${TAG}_$c.log 2>&1 || { echo "pmc $c failed"; tail -5 gpurun_out/pmc_${TAG}_$c.log; exit 6; }
 done
