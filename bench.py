@@ -279,6 +279,15 @@ def main():
                  'peak_tflops': FP64_PEAK_TFLOPS}
         if integ['achieved_tflops'] is not None:
             integ['frac'] = integ['achieved_tflops'] / FP64_PEAK_TFLOPS
+            # the agent state is streamed once per step: at a few flops per byte
+            # (small networks) the launch is HBM-bound, not FP64-bound
+            bpa = col.engine.dopri5_bytes_per_agent_step()
+            gbps = (agent_steps / args.steps) * bpa / (kin_ms * 1e-3) / 1e9
+            t_flop = integ_flops / (FP64_PEAK_TFLOPS * 1e12)
+            t_byte = (agent_steps / args.steps) * bpa / (HBM_PEAK_GBPS * 1e9)
+            integ.update({'bytes_per_agent_step': bpa, 'achieved_gbps': gbps,
+                          'roofline_bound': 'fp64' if t_flop >= t_byte else 'hbm',
+                          'roofline_frac': max(t_flop, t_byte) / (kin_ms * 1e-3)})
         roofline = None
         if lat is not None:
             # dominant kernel: one fused pass of `depth` substeps (k_diffuse_wt<depth>)

@@ -17,7 +17,8 @@ import os
 
 from lens_amd.rate_law_compiler import RateLawTable
 
-TEMPLATE = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'csrc', 'vk_dopri5_spec.hip.in')
+TEMPLATE = os.environ.get('VK_DOPRI5_TEMPLATE') or os.path.join(os.path.dirname(os.path.abspath(__file__)), 'csrc',
+                                                                 'vk_dopri5_spec.hip.in')
 
 
 def _f(x: float) -> str:
@@ -44,7 +45,7 @@ def rhs_body(t: RateLawTable) -> str:
             terms = ['fma(c[%d], p[%d], 1.0)' % (t.mem_species[m], t.mem_param[m])
                      for m in range(t.set_ptr[s], t.set_ptr[s + 1])]
             lines.append('        den += %s - 1.0;' % (' * '.join(terms) if terms else '1.0'))
-        lines.append('        f%d += num / den;' % t.rl_reaction[l])
+        lines.append('        f%d += vk_div(num, den);' % t.rl_reaction[l])
         lines.append('    }')
     for i in range(nd):
         expr = '0.0'

@@ -393,6 +393,26 @@ constexpr double b1 = 35.0 / 384.0, b3 = 500.0 / 1113.0, b4 = 125.0 / 192.0,
 constexpr double e1 = 71.0 / 57600.0, e3 = -71.0 / 16695.0, e4 = 71.0 / 1920.0,
                  e5 = -17253.0 / 339200.0, e6 = 22.0 / 525.0, e7 = -1.0 / 40.0;
 constexpr double SAFETY = 0.9, MIN_FACTOR = 0.2, MAX_FACTOR = 10.0;
+
+// The adaptive kernels are tolerance-parity (within 1e-6 of odeint, SURVEY
+// 8a), not bit-parity, so they use the cheap forms of their two costliest
+// operations; the specialised kernel (vk_dopri5_spec.hip.in) uses the same
+// two, so it stays bit-identical to the table walk.
+// a/b by the hardware reciprocal plus two Newton steps (within an ulp or so;
+// a zero divisor gives NaN instead of inf -- flagged non-finite either way).
+__device__ __forceinline__ double fdiv(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return a * r;
+}
+
+// en^-0.2 for the step-size factor as exp2(-0.2 log2 en) in double: within a
+// few ulp of scipy's en ** -0.2, without pow()'s special-case handling (en is
+// finite and > 0 here).
+__device__ __forceinline__ double step_pow(double en) {
+    return exp2(-0.2 * log2(en));
+}
 }  // namespace dp
 
 constexpr int DP_BS = 256;
@@ -419,7 +439,7 @@ __device__ __forceinline__ double rate_law_tile(const vk_dev_table &t, int l, co
             term *= fma(cl[TI(t, mem_species, m) * DP_BS + lane], pl[TI(t, mem_param, m) * DP_BS + lane], 1.0);
         den += term - 1.0;
     }
-    return num / den;
+    return dp::fdiv(num, den);
 }
 
 template <int NY>
@@ -562,14 +582,14 @@ __global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t
             if (i < ny) {
                 const double err = hs * fma(dp::e7, k7[i], fma(dp::e6, k6[i], fma(dp::e5, k5[i],
                                        fma(dp::e4, k4[i], fma(dp::e3, k3[i], dp::e1 * k1[i])))));
-                const double q = err / fma(fmax(fabs(y[i]), fabs(yt[i])), rtol, atol);
+                const double q = dp::fdiv(err, fma(fmax(fabs(y[i]), fabs(yt[i])), rtol, atol));
                 en = fma(q, q, en);
             }
         }
         en = sqrt(en / ny);
         if (!isfinite(en)) { st |= VK_AGENT_NONFINITE; break; }
         if (en < 1.0) {
-            double factor = (en == 0.0) ? dp::MAX_FACTOR : fmin(dp::MAX_FACTOR, dp::SAFETY * pow(en, -0.2));
+            double factor = (en == 0.0) ? dp::MAX_FACTOR : fmin(dp::MAX_FACTOR, dp::SAFETY * dp::step_pow(en));
             if (rejected) factor = fmin(1.0, factor);
             tt = last ? dt : tt + hs;
 #pragma unroll
@@ -578,7 +598,7 @@ __global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t
             h = hs * factor;
             rejected = false;
         } else {
-            h = hs * fmax(dp::MIN_FACTOR, dp::SAFETY * pow(en, -0.2));
+            h = hs * fmax(dp::MIN_FACTOR, dp::SAFETY * dp::step_pow(en));
             rejected = true;
         }
     }
@@ -667,7 +687,7 @@ __device__ __forceinline__ double rate_law_wave(const vk_dev_table &t, const int
         for (int m = m0; m < m1; ++m) term *= fma(cl[ib[t.o_mem_species + m]], pl[ib[t.o_mem_param + m]], 1.0);
         den += term - 1.0;
     }
-    return num / den;
+    return dp::fdiv(num, den);
 }
 
 template <int NSLOT>
@@ -824,14 +844,14 @@ __global__ __launch_bounds__(DW * DW_WAVES) void k_dopri5_wave(vk_dev_table t, i
             if (lane + DW * k < ny) {
                 const double err = hs * fma(dp::e7, k7[k], fma(dp::e6, k6[k], fma(dp::e5, k5[k],
                                        fma(dp::e4, k4[k], fma(dp::e3, k3[k], dp::e1 * k1[k])))));
-                const double q = err / fma(fmax(fabs(y[k]), fabs(yt[k])), rtol, atol);
+                const double q = dp::fdiv(err, fma(fmax(fabs(y[k]), fabs(yt[k])), rtol, atol));
                 e2 = fma(q, q, e2);
             }
         }
         const double en = sqrt(wave_sum(e2) / ny);
         if (!isfinite(en)) { st |= VK_AGENT_NONFINITE; break; }
         if (en < 1.0) {
-            double factor = (en == 0.0) ? dp::MAX_FACTOR : fmin(dp::MAX_FACTOR, dp::SAFETY * pow(en, -0.2));
+            double factor = (en == 0.0) ? dp::MAX_FACTOR : fmin(dp::MAX_FACTOR, dp::SAFETY * dp::step_pow(en));
             if (rejected) factor = fmin(1.0, factor);
             tt = last ? dt : tt + hs;
 #pragma unroll
@@ -840,7 +860,7 @@ __global__ __launch_bounds__(DW * DW_WAVES) void k_dopri5_wave(vk_dev_table t, i
             h = hs * factor;
             rejected = false;
         } else {
-            h = hs * fmax(dp::MIN_FACTOR, dp::SAFETY * pow(en, -0.2));
+            h = hs * fmax(dp::MIN_FACTOR, dp::SAFETY * dp::step_pow(en));
             rejected = true;
         }
     }
@@ -896,13 +916,13 @@ static int launch_dopri5_wave(const vk_table *t, int64_t n, int64_t ld, double d
         vk::set_error("vk_step_dopri5: agent-per-wavefront grid limited to 2^29 agents");
         return VK_ERR_LIMIT;
     }
+    auto kern = k_dopri5_wave<NSLOT>;
     if (lds > 64 * 1024)
-        (void)hipFuncSetAttribute((const void *)k_dopri5_wave<NSLOT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024);
+        (void)hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const unsigned blocks = (unsigned)((n + DW_WAVES - 1) / DW_WAVES);
-    hipLaunchKernelGGL(k_dopri5_wave<NSLOT>, dim3(blocks), dim3(DW * DW_WAVES), lds, stream, d, t->n_ib, t->n_db,
-                       tile, n, ld, dt, o->rtol, o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux,
-                       counts, status, nsteps);
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(DW * DW_WAVES), lds, stream, d, t->n_ib, t->n_db, tile, n, ld, dt,
+                       o->rtol, o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux, counts, status,
+                       nsteps);
     return vk::launch_check("k_dopri5_wave");
 }
 

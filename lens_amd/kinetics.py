@@ -157,3 +157,11 @@ class KineticsEngine:
         # solution (5 terms): 11, error (6 terms + h*): 12, norm: max/abs/fma/div/fma ~ 6
         per_component = 3 + 5 + 7 + 9 + 11 + 11 + 12 + 6
         return 6 * self.table.flops_rhs() + per_component * ny
+
+    def dopri5_bytes_per_agent_step(self) -> int:
+        """Algorithmic HBM bytes one agent-step of vk_step_dopri5 moves: reads
+        conc[S] + params[P] + mmol_to_counts + h_state, writes the integrated
+        rows [ND] + flux[R] + counts[n_ext] (int64) + h_state + status/nsteps (int32)."""
+        t = self.table
+        return 8 * (t.n_species + t.n_params + 2) + 8 * (t.n_dyn + t.n_reactions + t.n_ext + 1) + 8
+

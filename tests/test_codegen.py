@@ -37,7 +37,7 @@ def _py_rhs(t, conc, params):
         p[q] = 1.0 / p[q] if p[q] != 0 else 0.0
     c = list(conc)
     dy = [0.0] * (t.n_dyn + t.n_reactions)
-    env = {'c': c, 'p': p, 'dy': dy, 'fma': lambda a, b, d: a * b + d}
+    env = {'c': c, 'p': p, 'dy': dy, 'fma': lambda a, b, d: a * b + d, 'vk_div': lambda a, b: a / b}
     code = []
     for line in rhs_body(t).splitlines():
         s = line.strip()
