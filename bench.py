@@ -79,6 +79,8 @@ def parse():
                    help='output rows per wave tile (default 64 on one GPU, 0 = auto on row bands)')
     p.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
                    help='nccl (= RCCL) for real runs; gloo stages through host memory (rehearsal only)')
+    p.add_argument('--overlap-kinetics', action='store_true',
+                   help='run kinetics + gather on a side stream beside the diffusion passes')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -114,6 +116,7 @@ def build_rank(args, rank, world, dev):
     col = Colony(cfg, n_local, device=dev, integrator=args.integrator, environment=lat or 'held',
                  table=table, exchange=args.exchange, specialize=not args.generic_kernel, cells=cells,
                  capacity=int(n_local * 1.05) + 64 if cells is not None else None)
+    col.overlap_kinetics = bool(getattr(args, 'overlap_kinetics', False))
     col.set_agents(params=params, conc=conc, location=loc if nx else None)
     if cells is not None:
         # a colony spread over one generation: divisions every step from the start

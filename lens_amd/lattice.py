@@ -131,12 +131,22 @@ class Lattice:
             allreduce(self.uniform)
         return self.uniform
 
+    # substeps of the last launch that writes the field (one odd-depth pass;
+    # see vk_diffuse's pass planner) -- split off so that work on another
+    # stream that still READS the pre-step field can overlap all earlier passes
+    FINAL_SPLIT = 7
+
     def diffuse(self, timestep: float, halo_exchange: Optional[Callable] = None,
-                allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None):
+                allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None,
+                before_final: Optional[Callable] = None):
         """Advance every plane by ``timestep`` (diffusion_field.py:385-407).
 
         ``events`` = (start, end) torch.cuda.Events recorded on the launch
-        stream around the substep kernels only (bench roofline timing)."""
+        stream around the substep kernels only (bench roofline timing).
+        ``before_final`` is called (at enqueue time, on the host) before the
+        first launch that overwrites ``fields``: the caller makes the launch
+        stream wait there for readers of the pre-step field.  Every pass before
+        it reads ``fields`` and writes only the work planes."""
         n_sub = n_substeps(timestep, self.diffusion_dt)
         coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
         mm = self.uniform_summary(allreduce) if skip_uniform else None
@@ -153,7 +163,20 @@ class Lattice:
             cnt = min(k, n_sub - j)
             if banded:
                 halo_exchange(self.state_buffer(j), cnt)
-            self._run_block(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max)
+            split = 0
+            if before_final is not None and j + cnt == n_sub:
+                # unbanded: the planner's passes of [j, n_sub - 7) and [n_sub - 7, n_sub)
+                # are the same passes as for [j, n_sub) (e.g. 100 = 8x9 + 3x7 | 7);
+                # banded blocks are not split (their halo rows shrink over the block)
+                if not banded and cnt > 2 * self.FINAL_SPLIT:
+                    split = self.FINAL_SPLIT
+                if split:
+                    self._run_block(j, cnt - split, n_sub, coeff_dt, mm, lo_min, hi_max)
+                before_final()
+            if split:
+                self._run_block(j + cnt - split, split, n_sub, coeff_dt, mm, lo_min, hi_max)
+            else:
+                self._run_block(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max)
             j += cnt
         if events is not None:
             events[1].record()

@@ -436,6 +436,34 @@ def test_banded_diffusion_equals_whole(dev):
         assert np.array_equal(got, whole.owned('a').cpu().numpy()), (world, halo)
 
 
+def test_lattice_colony_side_stream_overlap_is_exact(dev):
+    """Kinetics + gather on the side stream beside the diffusion passes gives
+    the same fields and agent state, bit for bit, as the one-stream order."""
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    cfg = configs.glc_ac_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    nx, n = 256, 20000
+    rng = np.random.default_rng(21)
+    loc = rng.uniform(0, float(nx), (2, n))
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=5)
+    out = []
+    for overlap in (False, True):
+        lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (float(nx), float(nx)), 10.0, 5.0, device=dev,
+                      initial={'glc__D_e': configs.gaussian_bump_field((nx, nx)), 'ac_e': np.zeros((nx, nx))})
+        col = Colony(cfg, n, device=dev, integrator='dopri5', environment=lat, table=t, specialize=True)
+        col.overlap_kinetics = overlap
+        col.set_agents(params=params, conc=conc, location=loc)
+        col.gather_external()
+        for _ in range(3):
+            col.step(1.0)
+        torch.cuda.synchronize()
+        out.append((lat.owned('glc__D_e').cpu().numpy(), lat.owned('ac_e').cpu().numpy(),
+                    col.conc[:, :n].cpu().numpy(), col.counts[:, :n].cpu().numpy()))
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+
+
 def test_lattice_colony_step_vs_oracle(dev):
     """Gather (pre-step) -> diffusion -> agent-ordered exchange, bit-exact, with a
     bin shared by several agents."""
