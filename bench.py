@@ -233,16 +233,16 @@ def main():
         torch.cuda.synchronize()
 
     ev = lambda: torch.cuda.Event(enable_timing=True)
-    timing = [{'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())}
-              for _ in range(max(args.steps, args.warmup))]
-    nsteps_acc = torch.zeros((), dtype=torch.int64, device=dev)
+    mk = lambda: ({'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())})
+    timing = [mk() for _ in range(args.steps)]          # timed steps only
+    warm_timing = [mk() for _ in range(args.warmup)]
+    col.count_attempts(True)
     # warmup runs exactly the timed loop body (first-use costs land here)
     for k in range(args.warmup):
-        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing[k])
-        nsteps_acc += col.nsteps[:col.n].sum()
+        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=warm_timing[k])
     barrier()
     col.check_status()
-    nsteps_acc.zero_()
+    col.attempts.zero_()
     agent_steps = 0          # agents integrated, summed over the timed steps (divisions grow n)
     n_start = col.n
     barrier()
@@ -250,7 +250,6 @@ def main():
     for k in range(args.steps):
         agent_steps += col.n
         col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing[k])
-        nsteps_acc += col.nsteps[:col.n].sum()
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()
@@ -260,7 +259,7 @@ def main():
     kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
     diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
                if lat is not None else 0.0)
-    attempts = float(nsteps_acc.item())
+    attempts = float(col.attempts.item())
     if dist is not None:
         if args.dist_backend == 'gloo':
             el, n_agents = el.cpu(), n_agents.cpu()

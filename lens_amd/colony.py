@@ -59,7 +59,7 @@ class Colony:
             raise ValueError('exchange must be sorted or atomic')
         self.config = config
         self.table = table or compile_rate_laws(config['reactions'], config['kinetic_parameters'])
-        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.device = native.resolve_device(device)
         # lattice colonies: optionally run kinetics + gather on a side stream
         # beside the diffusion passes (step()); results are identical either way.
         # Off by default: on one MI355X the C4 stencil passes already fill the
@@ -189,6 +189,13 @@ class Colony:
                 native.stream_handle()), 'vk_gather')
 
     # -- one timestep -------------------------------------------------------------
+    def count_attempts(self, on: bool = True):
+        """Accumulate DP45 attempts (accepted + rejected steps) of every agent
+        into ``self.attempts`` (device int64), summed right after the kinetics
+        launch -- before division copies a mother's ``nsteps`` into both
+        daughters (bench flop accounting)."""
+        self.attempts = torch.zeros((), dtype=torch.int64, device=self.device) if on else None
+
     def kinetics(self, dt: float):
         if self.integrator == 'euler':
             self.engine.euler(dt, self.params, self.conc, self.m2c, self.n, self.flux, self.counts,
@@ -197,6 +204,8 @@ class Colony:
             self.engine.dopri5(dt, self.params, self.conc, self.m2c, self.n, self.h_state, self.rtol,
                                self.atol, self.max_steps, self.flux, self.counts, self.status,
                                self.nsteps)
+            if getattr(self, 'attempts', None) is not None:
+                self.attempts += self.nsteps[:self.n].sum()
 
     def step(self, dt: float = 1.0, halo_exchange=None, allreduce=None, timing=None):
         """One timestep.  ``timing`` (optional) = {'kin': (ev0, ev1), 'diff': (ev0, ev1)}

@@ -32,8 +32,8 @@ constexpr int ST_RB = 16;   // rows walked per block
 // column keeping up/centre/down in registers: one new row load, two shifted
 // loads (left/right: L1 hits on the lines the wave just fetched), one store.
 __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restrict__ src,
-                                                           double *__restrict__ dst,
-                                                           const double *__restrict__ f0,
+                                                           double *dst,
+                                                           const double *f0,
                                                            int64_t field_stride, int ny, int lo, int hi,
                                                            int top_reflect, int bot_reflect, double coef,
                                                            const double *__restrict__ uniform) {
@@ -89,7 +89,7 @@ extern "C" int vk_set_stencil_depth(int32_t k) {
 }
 
 // rows [lo, hi) of every non-uniform plane: dst <- src
-__global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ src, double *__restrict__ dst,
+__global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ src, double *dst,
                                                    int64_t field_stride, int64_t off, int64_t count,
                                                    const double *__restrict__ uniform) {
     const int f = blockIdx.y;
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void k_gather(const double *__restrict__ field
                                                 const int32_t *__restrict__ bin_lin, int64_t n,
                                                 const int32_t *__restrict__ map_field,
                                                 const int32_t *__restrict__ map_row, int n_map,
-                                                double *__restrict__ dst, int64_t ld) {
+                                                double *dst, int64_t ld) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= n) return;
     const int64_t b = bin_lin[a];

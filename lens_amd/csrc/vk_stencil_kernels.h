@@ -39,7 +39,7 @@ constexpr int TB_BX = 256;
 template <int K, bool EDGE, int U>
 __device__ __forceinline__ void tb_iter(double (&xch)[2][K][TB_BX], double (&X0)[K], double (&X1)[K],
                                         double (&X2)[K], double (&pf)[3], const double *__restrict__ s,
-                                        double *__restrict__ d, const double *__restrict__ g, int ny, int i,
+                                        double *d, const double *g, int ny, int i,
                                         int c0, int c1, int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                         int c, int cc, bool writer, int tl, int tr, bool left_edge,
                                         bool right_edge, double coef) {
@@ -80,7 +80,7 @@ __device__ __forceinline__ void tb_iter(double (&xch)[2][K][TB_BX], double (&X0)
 // interior tiles (the vast majority) carry no boundary selects at all.
 template <int K, bool EDGE>
 __device__ __forceinline__ void diffuse_tb_body(double (&xch)[2][K][TB_BX], const double *__restrict__ s,
-                                                double *__restrict__ d, const double *__restrict__ g, int ny,
+                                                double *d, const double *g, int ny,
                                                 int c0, int c1, int in_lo, int in_hi, int top_reflect,
                                                 int bot_reflect, int x0, double coef) {
     const int tid = threadIdx.x;
@@ -111,8 +111,8 @@ __device__ __forceinline__ void diffuse_tb_body(double (&xch)[2][K][TB_BX], cons
 }
 
 template <int K>
-__global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__ src, double *__restrict__ dst,
-                                                      const double *__restrict__ f0, int64_t field_stride, int ny,
+__global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__ src, double *dst,
+                                                      const double *f0, int64_t field_stride, int ny,
                                                       int out_lo, int out_hi, int in_lo, int in_hi,
                                                       int top_reflect, int bot_reflect, int rows_per_chunk,
                                                       double coef, const double *__restrict__ uniform) {
@@ -204,8 +204,8 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
 // so the K stages are straight-line code the scheduler can interleave.
 template <int K, bool EDGE, bool FINAL, bool STEADY, int U>
 __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], double2 (&X2)[K], double2 (&pf)[3],
-                                        const double *__restrict__ s, double *__restrict__ d,
-                                        const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                        const double *__restrict__ s, double *d,
+                                        const double *g, const WtLane &L, int i, int c0, int c1,
                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
     double2(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
     double2(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
@@ -253,8 +253,8 @@ __device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], doub
 }
 
 template <int K, bool EDGE, bool FINAL>
-__device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, double *__restrict__ d,
-                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+__device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, double *d,
+                                                const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef) {
     double2 X0[K], X1[K], X2[K], pf[3];
@@ -283,8 +283,8 @@ __device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, do
 }
 
 template <int K, bool FINAL>
-__global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ src, double *__restrict__ dst,
-                                                    const double *__restrict__ f0, int64_t field_stride, int ny,
+__global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ src, double *dst,
+                                                    const double *f0, int64_t field_stride, int ny,
                                                     int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
                                                     int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
                                                     int n_fields, double coef, const double *__restrict__ uniform) {
@@ -337,8 +337,8 @@ __global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ s
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
 template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U>
 __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
-                                        const double *__restrict__ s, double *__restrict__ d,
-                                        const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                        const double *__restrict__ s, double *d,
+                                        const double *g, const WtLane &L, int i, int c0, int c1,
                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
     constexpr int R = U % 3;
     double2(&UP)[K] = R == 0 ? S0 : (R == 1 ? S1 : S2);
@@ -390,8 +390,8 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
 
 template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
-                                         double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *__restrict__ d,
-                                         const double *__restrict__ g, const WtLane &L, int i, int c0, int c1,
+                                         double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *d,
+                                         const double *g, const WtLane &L, int i, int c0, int c1,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
     wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect,
                                         bot_reflect, coef);
@@ -403,8 +403,8 @@ __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], dou
 template <int K, int PD, bool EDGE, bool FINAL, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
                                                 double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
-                                                const double *__restrict__ s, double *__restrict__ d,
-                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+                                                const double *__restrict__ s, double *d,
+                                                const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef) {
     const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
@@ -422,8 +422,8 @@ __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...
 }
 
 template <int K, int PD, bool EDGE, bool FINAL>
-__device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *__restrict__ d,
-                                                const double *__restrict__ g, const WtLane &L, int c0, int c1,
+__device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *d,
+                                                const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef) {
     double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
@@ -445,8 +445,8 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
 }
 
 template <int K, int PD, bool FINAL>
-__device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *__restrict__ dst,
-                                                const double *__restrict__ f0, int64_t field_stride, int ny,
+__device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *dst,
+                                                const double *f0, int64_t field_stride, int ny,
                                                 int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
                                                 int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
                                                 int n_fields, double coef, const double *__restrict__ uniform) {
@@ -487,8 +487,11 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
         diffuse_wl_body<K, PD, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
+// Aliasing: the FINAL pass writes the field it also reads as the base plane
+// (dst == f0, vk_diffuse), so only the source plane is __restrict__; each base
+// load feeds the store of the same cell, later in program order.
 #define VK_WL_PARAMS                                                                                           \
-    const double *__restrict__ src, double *__restrict__ dst, const double *__restrict__ f0, int64_t field_stride, \
+    const double *__restrict__ src, double *dst, const double *f0, int64_t field_stride, \
         int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect, int bot_reflect, int rows_per_chunk, \
         int tiles_x, int chunks_y, int n_fields, double coef, const double *__restrict__ uniform
 #define VK_WL_ARGS                                                                                             \

@@ -41,6 +41,8 @@ def make_halo_exchange(lat, rank: int, world: int, group=None):
     neighbouring ranks' owned rows."""
     h = lat.halo
     owned = lat.row_hi - lat.row_lo
+    if h < 1 and not (lat.edge_top and lat.edge_bot):
+        raise ValueError('a multi-rank row band needs halo >= 1 (got %d)' % h)
     if h > owned:
         raise ValueError('halo (%d) deeper than the band (%d rows)' % (h, owned))
     nf, ny = len(lat.molecules), lat.ny

@@ -202,7 +202,7 @@ class ExpressionEngine:
     def __init__(self, table: ExpressionTable, device=None):
         native.load()
         self.table = table
-        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.device = native.resolve_device(device)
         self._dev = {k: torch.from_numpy(np.ascontiguousarray(getattr(table, k))).to(self.device)
                      for k in ('tx_row', 'tx_rate', 'tx_deg', 'tx_prog_ptr', 'code', 'thr', 'tl_row',
                                'tl_mrna_row', 'tl_rate', 'tl_deg')}

@@ -20,6 +20,7 @@ from typing import Dict, List, Tuple
 import numpy as np
 import torch
 
+from lens_amd import native
 from lens_amd.kinetics import KineticsEngine
 from lens_amd.process import BatchedConvenienceKinetics
 
@@ -27,7 +28,7 @@ _ENGINES: Dict[Tuple[str, int], KineticsEngine] = {}
 
 
 def engine_for(process: BatchedConvenienceKinetics, device=None) -> KineticsEngine:
-    dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+    dev = native.resolve_device(device)
     key = (process.signature, dev.index if dev.index is not None else 0)
     eng = _ENGINES.get(key)
     if eng is None:

@@ -37,7 +37,7 @@ class KineticsEngine:
 
     def __init__(self, table: RateLawTable, device=None):
         self.table = table
-        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.device = native.resolve_device(device)
         with torch.cuda.device(self.device):
             self.dev = native.DeviceTable(table)
         self.specialized = False

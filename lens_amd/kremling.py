@@ -61,7 +61,7 @@ class KremlingColony:
     def __init__(self, n_agents: int, device=None, parameters=None, internal=None, external=None,
                  volume_fl: float = 1.0, rtol: float = 1e-8, atol: float = 1e-12, max_steps: int = 1_000_000,
                  avogadro: float = N_A_LEGACY):
-        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.device = native.resolve_device(device)
         native.load()
         self.n = int(n_agents)
         self.parameters = dict(KREMLING_PARAMETERS, **(parameters or {}))

@@ -57,7 +57,7 @@ class Lattice:
         self.depth = float(depth)
         self.avogadro = float(avogadro)
         nx, ny = self.n_bins
-        self.device = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        self.device = native.resolve_device(device)
         # DiffusionField.__init__ (diffusion_field.py:251-260)
         dx = self.bounds[0] / nx
         dy = self.bounds[1] / ny
@@ -73,6 +73,12 @@ class Lattice:
         self.halo = int(halo)
         self.edge_top = lo == 0
         self.edge_bot = hi == nx
+        if not (self.edge_top and self.edge_bot) and self.halo < 1:
+            # an interior band edge without halo rows would act as a reflecting
+            # wall: the field would silently stop coupling across ranks
+            raise ValueError('a row band %r of %d rows needs halo >= 1 (got %d)' % ((lo, hi), nx, self.halo))
+        if self.halo > hi - lo and not (self.edge_top and self.edge_bot):
+            raise ValueError('halo (%d) deeper than the band (%d rows)' % (self.halo, hi - lo))
         h = self.halo
         self.pad_top = 0 if self.edge_top else h
         self.pad_bot = 0 if self.edge_bot else h

@@ -151,6 +151,20 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+def resolve_device(device=None):
+    """torch.device with an explicit index: ``'cuda'`` -> ``cuda:<current>``.
+
+    Tensors always report an indexed device, and ``cuda != cuda:0`` in torch,
+    so every engine keeps the indexed form (Colony(device='cuda'))."""
+    import torch
+    if device is None:
+        return torch.device('cuda', torch.cuda.current_device())
+    d = torch.device(device)
+    if d.type == 'cuda' and d.index is None:
+        return torch.device('cuda', torch.cuda.current_device())
+    return d
+
+
 def stream_handle(stream=None) -> int:
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()

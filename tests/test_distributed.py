@@ -124,3 +124,16 @@ def test_row_bands_cover_exactly():
             assert b[0][0] == 0 and b[-1][1] == nx
             assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
             assert max(h - l for l, h in b) - min(h - l for l, h in b) <= 1
+
+
+def test_interior_band_without_halo_is_rejected():
+    """an interior band edge with halo 0 would act as a reflecting
+    wall and silently decouple the ranks' fields."""
+    with pytest.raises(ValueError):
+        Lattice(['a'], (41, 23), (41.0, 23.0), 10.0, 5.0, device='cpu', row_band=(0, 20), halo=0)
+    with pytest.raises(ValueError):
+        Lattice(['a'], (41, 23), (41.0, 23.0), 10.0, 5.0, device='cpu', row_band=(20, 41), halo=0)
+    with pytest.raises(ValueError):   # halo deeper than the band
+        Lattice(['a'], (41, 23), (41.0, 23.0), 10.0, 5.0, device='cpu', row_band=(20, 25), halo=8)
+    # the whole domain as one band needs no halo
+    Lattice(['a'], (41, 23), (41.0, 23.0), 10.0, 5.0, device='cpu', row_band=(0, 41), halo=0)
