@@ -87,7 +87,10 @@ def parse():
 
 
 def build_rank(args, rank, world, dev):
+    """This rank's share of the workload: (colony, lattice or None, host inputs).
+    ``args.agents`` (optional) overrides the agent count (tests)."""
     n_total, nx, bound, _ = WORKLOADS[args.workload]
+    n_total = getattr(args, 'agents', None) or n_total
     cells = None
     if args.workload == 'c5':
         from lens_amd.cells import CellModel

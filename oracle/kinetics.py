@@ -185,3 +185,20 @@ class OracleODE:
                     name = port_state[1]
                     counts[name] = counts.get(name, 0) + int(coeff * y[nd + r] * m2c)
         return new, fluxes, counts
+
+
+def params_dict(param_names, config, pvec):
+    """Per-agent parameter vector (RateLawTable.param_names order) -> a
+    reference ``kinetic_parameters`` dict ({rxn: {enzyme: {mol: Km, 'kcat_f':
+    kcat}}}); ``None`` Kms of the configuration are kept (they are not table
+    parameters)."""
+    kp = {}
+    for (kind, rid, enz, *mol), v in zip(param_names, pvec):
+        kp.setdefault(rid, {}).setdefault(enz, {})
+        kp[rid][enz]['kcat_f' if kind == 'kcat' else mol[0]] = float(v)
+    for rid in config['kinetic_parameters']:
+        for enz, p in config['kinetic_parameters'][rid].items():
+            for k, v in p.items():
+                if v is None:
+                    kp[rid][enz][k] = None
+    return kp

@@ -1,0 +1,437 @@
+"""BASELINE configs 2-5 at their own size, HIP path vs the oracle (needs an MI355X).
+
+Every colony here is built by ``bench.build_rank`` -- the exact workload the
+headline benchmark times -- and checked against the C restatement in
+``oracle/cpu_kinetics.c`` (DP45 / Euler / stencil / agent-ordered exchange)
+and the SoA division oracle in ``oracle/colony.py``:
+
+* C2 (10k heterogeneous agents, held externals, 100 steps): every agent, every
+  step vs the C oracle; a 304-agent sample's 100-step trajectory vs scipy
+  odeint (``tests/golden/c2_odeint_traj.npz``, made by
+  ``tests/golden/make_c2_odeint.py``).
+* C3 (100k agents, 1024^2, glucose + acetate): 5 Euler steps free-running,
+  bit for bit; 5 DP45 steps, each from the GPU's step-start state.
+* C4 (1M agents, 4096^2 x 2): one full step, Euler bit for bit and DP45, plus
+  the per-bin exchange-conservation property.
+* C5 (50-species network, agent-per-wavefront DP45, Growth + DeriveGlobals +
+  DivisionVolume division): 20 steps at 4096 agents vs both oracles, and one
+  full 1M-agent step (every agent's division bookkeeping bit for bit, a
+  kinetics sample vs the C oracle).
+
+Tolerances (north star: end states within 1e-6 relative of odeint):
+  GPU DP45 vs the C oracle (same algorithm): 1e-9 relative per species, the
+  scale floored at 1e-9 x the species' largest magnitude (species driven
+  through zero); exchange counts equal except a one-count truncation flip
+  where a flux integral sits on an integer boundary.
+  GPU DP45 vs odeint: 1e-6 relative + 1e-10 absolute.
+  Euler, stencil, exchange, gather, division: bit for bit.
+"""
+
+import os
+import sys
+import types
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+
+import bench  # noqa: E402
+from oracle import colony as oc  # noqa: E402
+from oracle import cpu  # noqa: E402
+from lens_amd.lattice import n_substeps  # noqa: E402
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda', 0)
+
+
+def _args(workload, integrator='dopri5', agents=None):
+    return types.SimpleNamespace(workload=workload, integrator=integrator, halo=0, exchange='sorted',
+                                 generic_kernel=False, agents=agents, overlap_kinetics=False)
+
+
+def _pull(col, lat=None):
+    n = col.n
+    h = lambda t: t[..., :n].cpu().numpy().copy()
+    s = types.SimpleNamespace(n=n, conc=h(col.conc), params=h(col.params), m2c=h(col.m2c),
+                              h=h(col.h_state), counts=h(col.counts), nsteps=h(col.nsteps),
+                              ids=col.agent_ids())
+    if col.cells is not None:
+        s.cell = h(col.cell)
+    if lat is not None:
+        s.fields = [lat.owned(m).cpu().numpy().copy() for m in lat.molecules]
+        s.loc = h(col.location)
+        s.bin_lin = h(col.bin_lin)
+    return s
+
+
+def _bins(loc, lat):
+    """get_bin_site (lattice_utils.py:34-40) on every agent, as linear bins."""
+    nx, ny = lat.n_bins
+    bx, by = lat.bounds
+    i = np.mod(np.floor(loc[0] * nx / bx).astype(np.int64), nx)
+    j = np.mod(np.floor(loc[1] * ny / by).astype(np.int64), ny)
+    return (i * ny + j).astype(np.int32)
+
+
+def _rel_close(got, ref, tol, frac=1e-4, north_star=True):
+    """Relative error per element (scale floored at 1e-9 x the row's largest
+    magnitude) below ``tol`` for all but a fraction ``frac`` of the agents --
+    where the two implementations' rounding tips a borderline accept/reject
+    decision of the adaptive step control, the trajectories legitimately part
+    at the rtol level -- and every element within the north-star bound
+    |got - ref| <= 1e-6 |ref| + 1e-10."""
+    scale = np.abs(ref) + 1e-9 * np.abs(ref).max(axis=-1, keepdims=True) + 1e-300
+    err = np.abs(got - ref) / scale
+    per_agent = err.max(axis=0) if err.ndim == 2 else err
+    if north_star:
+        over = np.abs(got - ref) - (1e-6 * np.abs(ref) + 1e-10)
+        assert over.max() <= 0, float(over.max())
+    assert np.count_nonzero(per_agent >= tol) <= max(3, frac * per_agent.size), (
+        np.count_nonzero(per_agent >= tol), float(np.sort(per_agent)[-1]))
+
+
+def _oracle_kinetics(t, integrator, pre, cols=None):
+    """The C oracle's kinetics step from a step-start state; returns (conc, flux, counts, h, nsteps)."""
+    sl = slice(None) if cols is None else cols
+    params = np.ascontiguousarray(pre.params[:, sl])
+    conc = np.ascontiguousarray(pre.conc[:, sl])
+    m2c = np.ascontiguousarray(pre.m2c[sl])
+    desc = cpu.Desc(t)
+    if integrator == 'euler':
+        flux, counts = cpu.step_euler(desc, 1.0, params, conc, m2c)
+        return conc, flux, counts, None, None
+    h = np.ascontiguousarray(pre.h[sl])
+    flux, counts, status, nsteps = cpu.step_dopri5(desc, 1.0, params, conc, m2c, h_state=h)
+    assert not status.any()
+    return conc, flux, counts, h, nsteps
+
+
+def _oracle_lattice(col, lat, fields, bins, counts):
+    """diffusion_delta (100 substeps, uniform skip) then the exchange in agent order
+    (registry.py:149-183); returns (new fields, diffused fields)."""
+    t = col.table
+    coef = lat.diffusion * lat.diffusion_dt
+    out = []
+    for f in fields:
+        g = np.ascontiguousarray(f.copy())
+        cpu.diffuse(g, coef, n_substeps(1.0))
+        out.append(g)
+    diffused = [g.copy() for g in out]
+    for e, mol in enumerate(t.external_ids):
+        if mol in lat.molecules:
+            cpu.exchange(out[lat.molecules.index(mol)].reshape(-1), bins, counts[e], lat.binvol_avogadro)
+    return out, diffused
+
+
+def _check_counts(got, ref):
+    d = got.astype(np.int64) - ref.astype(np.int64)
+    assert np.abs(d).max() <= 1
+    assert np.count_nonzero(d) <= max(3, 1e-4 * d.size), np.count_nonzero(d)
+
+
+def _check_lattice_step(col, lat, pre, post, integrator, ref_counts):
+    """One lattice colony step: bins, one-step-lag gather, stencil + exchange bit for bit,
+    per-bin count conservation."""
+    t = col.table
+    bins = _bins(pre.loc, lat)
+    assert np.array_equal(bins, pre.bin_lin)
+    # get_local_environments: external := the PRE-step field at the agent's bin
+    for f, mol in enumerate(lat.molecules):
+        key = ('external', mol)
+        if key in t.species:
+            assert np.array_equal(post.conc[t.species.index(key)], pre.fields[f].reshape(-1)[bins]), mol
+    if integrator == 'euler':
+        assert np.array_equal(post.counts, ref_counts)
+    else:
+        _check_counts(post.counts, ref_counts)
+    new, diffused = _oracle_lattice(col, lat, pre.fields, bins, post.counts)
+    for f, mol in enumerate(lat.molecules):
+        assert np.array_equal(post.fields[f], new[f]), mol
+    # conservation: per bin, the exchanged concentration is the sum of its agents' counts
+    for e, mol in enumerate(t.external_ids):
+        f = lat.molecules.index(mol)
+        want = np.zeros(lat.n_bins[0] * lat.n_bins[1], dtype=np.int64)
+        np.add.at(want, bins, post.counts[e])
+        got = np.rint((post.fields[f] - diffused[f]).reshape(-1) * lat.binvol_avogadro / 1000.0)
+        assert np.array_equal(got.astype(np.int64), want), mol
+
+
+# ---------------------------------------------------------------------------
+# C4: 1M agents + 4096 x 4096 x 2 fields, one full step
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize('integrator', ['euler', 'dopri5'])
+def test_c4_full_step_vs_c_oracle(dev, integrator):
+    col, lat, _ = bench.build_rank(_args('c4', integrator), 0, 1, dev)
+    assert col.n == 1_000_000 and lat.n_bins == [4096, 4096] and len(lat.molecules) == 2
+    pre = _pull(col, lat)
+    col.step(1.0)
+    col.check_status()
+    torch.cuda.synchronize()
+    post = _pull(col, lat)
+    conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, integrator, pre)
+    nd = col.table.n_dyn
+    if integrator == 'euler':
+        assert np.array_equal(post.conc[:nd], conc[:nd])
+    else:
+        _rel_close(post.conc[:nd], conc[:nd], 1e-9)
+        assert np.mean(post.nsteps == nsteps) > 0.99
+    _check_lattice_step(col, lat, pre, post, integrator, counts)
+
+
+# ---------------------------------------------------------------------------
+# C3: 100k agents + 1024 x 1024 x 2 fields
+# ---------------------------------------------------------------------------
+
+def test_c3_euler_five_steps_free_running_bitwise(dev):
+    """The oracle runs on its own state for 5 steps (one-step external lag,
+    diffusion, agent-ordered exchange); the GPU must equal it bit for bit."""
+    col, lat, _ = bench.build_rank(_args('c3', 'euler'), 0, 1, dev)
+    assert col.n == 100_000 and lat.n_bins == [1024, 1024]
+    t = col.table
+    ref = _pull(col, lat)
+    bins = _bins(ref.loc, lat)
+    ext_rows = [(t.species.index(('external', m)), f) for f, m in enumerate(lat.molecules)
+                if ('external', m) in t.species]
+    for step in range(5):
+        conc, flux, counts, _, _ = _oracle_kinetics(t, 'euler', ref)
+        for row, f in ext_rows:
+            conc[row] = ref.fields[f].reshape(-1)[bins]      # pre-step field (one-step lag)
+        fields, _ = _oracle_lattice(col, lat, ref.fields, bins, counts)
+        ref.conc, ref.fields = conc, fields
+        col.step(1.0)
+        post = _pull(col, lat)
+        assert np.array_equal(post.counts, counts), step
+        assert np.array_equal(post.conc, ref.conc), step
+        for f in range(len(fields)):
+            assert np.array_equal(post.fields[f], fields[f]), (step, f)
+
+
+def test_c3_dopri5_five_steps_vs_c_oracle(dev):
+    """5 DP45 steps; each step checked against the oracle run from the GPU's
+    step-start state (agents to 1e-9, lattice bit for bit given the counts)."""
+    col, lat, _ = bench.build_rank(_args('c3', 'dopri5'), 0, 1, dev)
+    nd = col.table.n_dyn
+    for step in range(5):
+        pre = _pull(col, lat)
+        col.step(1.0)
+        col.check_status()
+        post = _pull(col, lat)
+        conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, 'dopri5', pre)
+        _rel_close(post.conc[:nd], conc[:nd], 1e-9)
+        _rel_close(post.h, h, 1e-3, frac=1e-2, north_star=False)   # step-size carry: heuristic
+        _check_lattice_step(col, lat, pre, post, 'dopri5', counts)
+
+
+# ---------------------------------------------------------------------------
+# C2: 10k heterogeneous agents, held externals
+# ---------------------------------------------------------------------------
+
+def test_c2_hundred_steps_every_agent_vs_c_oracle(dev):
+    col, _, _ = bench.build_rank(_args('c2', 'dopri5'), 0, 1, dev)
+    assert col.n == 10_000
+    nd = col.table.n_dyn
+    for step in range(100):
+        pre = _pull(col)
+        col.step(1.0)
+        post = _pull(col)
+        conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, 'dopri5', pre)
+        _rel_close(post.conc[:nd], conc[:nd], 1e-9)
+        _check_counts(post.counts, counts)
+        assert np.array_equal(post.conc[nd:], pre.conc[nd:])        # held externals / enzymes
+    col.check_status()
+
+
+def _fixture_case(name):
+    sys.path.insert(0, GOLDEN)
+    import make_odeint_traj as mk
+    return mk.CASES[name], mk._setup(name)
+
+
+@pytest.mark.parametrize('name', ['c2', 'c3kin', 'c5kin'])
+def test_trajectory_vs_odeint_fixture(dev, name):
+    """North-star bar over whole runs: consecutive one-second DP45 steps (rtol
+    1e-8, the bench setting) stay within 1e-6 relative (+1e-10 absolute) of
+    scipy odeint (LSODA, rtol 1e-12) restarted per step, for every agent of
+    the fixture's sample at every recorded step.  c2 = BASELINE config 2 (10k
+    glc_lct agents, 100 steps); c3kin = the C3/C4 kinetics (glc_ac, 100k
+    agents, 100 steps, held externals); c5kin = the stiff C5 network (4096
+    agents, agent-per-wavefront kernel, 10 steps)."""
+    from lens_amd.colony import Colony
+    z = np.load(os.path.join(GOLDEN, '%s_odeint_traj.npz' % name))
+    (_, n_agents, stride, _, steps, every), (cfg, t, params, conc) = _fixture_case(name)
+    sample = z['sample']
+    assert np.array_equal(sample, np.arange(0, n_agents, stride))
+    # the fixture was made from the same seeded colony
+    assert np.array_equal(params[:, sample], z['params']) and np.array_equal(conc[:, sample], z['conc'])
+    col = Colony(cfg, n_agents, device=dev, integrator='dopri5', environment='held', table=t, specialize=True)
+    col.set_agents(params=params, conc=conc)
+    assert float(col.m2c[0]) == float(z['m2c'])
+    nd = t.n_dyn
+    k = 0
+    for step in range(1, steps + 1):
+        col.step(1.0)
+        if step % every == 0:
+            got = col.conc[:nd].cpu().numpy()[:, sample].T          # [agent, species]
+            ref = z['y'][:, k]
+            err = np.abs(got - ref) - (1e-6 * np.abs(ref) + 1e-10)
+            assert err.max() <= 0, (step, float(err.max()))
+            fl = col.flux.cpu().numpy()[:, sample].T
+            ferr = np.abs(fl - z['flux'][:, k]) - (1e-6 * np.abs(z['flux'][:, k]) + 1e-10)
+            assert ferr.max() <= 0, (step, float(ferr.max()))
+            k += 1
+    col.check_status()
+
+
+# ---------------------------------------------------------------------------
+# C5: 50-species network + growth / DivisionVolume division
+# ---------------------------------------------------------------------------
+
+def _cell_dict(s):
+    from lens_amd import native
+    c = s.cell
+    return {'mass': c[native.VK_CELL_MASS].copy(), 'volume': c[native.VK_CELL_VOLUME].copy(),
+            'length': c[native.VK_CELL_LENGTH].copy(), 'surface_area': c[native.VK_CELL_SURFACE_AREA].copy(),
+            'protein': c[native.VK_CELL_PROTEIN].copy(), 'angle': c[native.VK_CELL_ANGLE].copy(),
+            'm2c': s.m2c.copy()}
+
+
+def _check_cells(post, ref_cell, ref_ids):
+    got = _cell_dict(post)
+    assert post.ids == ref_ids
+    for k in ('mass', 'volume', 'length', 'surface_area', 'protein', 'angle', 'm2c'):
+        assert np.array_equal(got[k], ref_cell[k]), k
+
+
+def test_c5_twenty_steps_vs_oracles(dev):
+    """Wave-DP45 kinetics + Growth/DeriveGlobals/DivisionVolume at 4096 agents:
+    per step, ids / order / cell rows bit for bit (SoA division oracle) and the
+    kinetics of every agent within 1e-9 of the C oracle (from the GPU's
+    step-start state), then gathered by the division order."""
+    col, _, _ = bench.build_rank(_args('c5', 'dopri5', agents=4096), 0, 1, dev)
+    cm = col.cells
+    assert col.engine.default_variant() == 1 and col.table.n_species >= 50
+    nd = col.table.n_dyn
+    divisions = 0
+    for step in range(20):
+        pre = _pull(col)
+        col.step(1.0)
+        col.check_status()
+        post = _pull(col)
+        conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, 'dopri5', pre)
+        cell, ids, order = oc.soa_step(_cell_dict(pre), pre.ids, 'growth', 1.0, rate=cm.growth_rate,
+                                       division_volume=cm.division_volume)
+        divisions += len(order) - pre.n
+        _check_cells(post, cell, ids)
+        _rel_close(post.conc[:nd], conc[:nd, order], 1e-9)
+        assert np.array_equal(post.params, pre.params[:, order])
+        assert np.array_equal(post.conc[nd:], pre.conc[nd:, order])
+        _check_counts(post.counts, counts[:, order])
+        _rel_close(post.h, h[order], 1e-3, frac=1e-2, north_star=False)
+    assert divisions >= 20, divisions
+
+
+def test_c5_full_size_step(dev):
+    """Second step of the 1M-agent C5 bench colony: every agent's growth, derived
+    globals and division bookkeeping bit for bit; kinetics of an 8192-agent
+    sample within 1e-9 of the C oracle."""
+    col, _, _ = bench.build_rank(_args('c5', 'dopri5'), 0, 1, dev)
+    cm = col.cells
+    assert col.n == 1_000_000
+    col.step(1.0)          # the colony starts just below the division volume: divisions from step 2
+    pre = _pull(col)
+    col.step(1.0)
+    col.check_status()
+    post = _pull(col)
+    cell, ids, order = oc.soa_step(_cell_dict(pre), pre.ids, 'growth', 1.0, rate=cm.growth_rate,
+                                   division_volume=cm.division_volume)
+    assert post.n == len(order) > pre.n
+    _check_cells(post, cell, ids)
+    sample = np.arange(8192)
+    conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, 'dopri5', pre, cols=sample)
+    # survivors keep their relative order: post column of pre agent a = its rank among survivors
+    keep = np.flatnonzero(np.bincount(order, minlength=pre.n) == 1)
+    pos = np.full(pre.n, -1)
+    pos[keep] = np.arange(len(keep))
+    ok = pos[sample] >= 0
+    nd = col.table.n_dyn
+    _rel_close(post.conc[:nd, pos[sample][ok]], conc[:nd][:, ok], 1e-9)
+
+
+# ---------------------------------------------------------------------------
+# DP45 lattice colony over 10 steps vs odeint + the lattice oracle
+# ---------------------------------------------------------------------------
+
+def test_lattice_colony_ten_dp45_steps_vs_odeint(dev):
+    """The C3/C4 step (kinetics with the one-step external lag, gather,
+    diffusion, agent-ordered exchange) for 10 steps against the Python oracle:
+    scipy odeint per agent (restated RHS, rtol 1e-12) + oracle.lattice.lattice_step.
+    Exchange counts may flip by one where a flux integral sits on an integer
+    boundary, which moves a bin by 1/(bin volume * N_A) mM: fields are compared
+    at 1e-6 relative, agents at the north-star 1e-6 relative + 1e-10."""
+    from lens_amd import configs
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    from lens_amd.rate_law_compiler import compile_rate_laws
+    from oracle import lattice as olat
+    from oracle.kinetics import OracleODE, mmol_to_counts, params_dict
+    cfg = configs.glc_ac_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    nx, ny, n = 24, 20, 60
+    bounds = (24.0, 20.0)
+    rng = np.random.default_rng(31)
+    loc = np.stack([rng.uniform(0, bounds[0], n), rng.uniform(0, bounds[1], n)])
+    loc[:, 7] = loc[:, 2]                                       # a shared bin
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=6)
+    glc = configs.gaussian_bump_field((nx, ny))
+    lat = Lattice(['glc__D_e', 'ac_e'], (nx, ny), bounds, 10.0, 5.0, device=dev,
+                  initial={'glc__D_e': glc, 'ac_e': np.zeros((nx, ny))})
+    col = Colony(cfg, n, device=dev, integrator='dopri5', environment=lat, table=t, specialize=True)
+    col.set_agents(params=params, conc=conc, location=loc)
+    col.gather_external()
+    m2c = mmol_to_counts()
+    assert float(col.m2c[0]) == m2c
+    odes = [OracleODE(cfg['reactions'], params_dict(t.param_names, cfg, params[:, a])) for a in range(n)]
+    fields = {'glc__D_e': glc.copy(), 'ac_e': np.zeros((nx, ny))}
+    locs = [tuple(loc[:, a]) for a in range(n)]
+    _, local = olat.lattice_step(fields, locs, {}, (nx, ny), bounds, 10.0, 0.0, 5.0)
+    agents = []
+    for a in range(n):
+        c = {k: conc[s, a] for s, k in enumerate(t.species)}
+        for m in fields:
+            c[('external', m)] = local[m][a]
+        agents.append(c)
+    for step in range(10):
+        counts = {m: [] for m in t.external_ids}
+        for a in range(n):
+            new, _, cnt = odes[a].step(agents[a], 1.0, m2c)
+            agents[a].update(new)
+            for m in t.external_ids:
+                counts[m].append(cnt.get(m, 0))
+        fields, local = olat.lattice_step(fields, locs, counts, (nx, ny), bounds, 10.0, 1.0, 5.0)
+        for a in range(n):
+            for m in fields:
+                agents[a][('external', m)] = local[m][a]
+        col.step(1.0)
+        col.check_status()
+        got = col.conc[:, :n].cpu().numpy()
+        for s, key in enumerate(t.species):
+            ref = np.array([agents[a][key] for a in range(n)])
+            assert (np.abs(got[s] - ref) <= 1e-6 * np.abs(ref) + 1e-10).all(), (step, key)
+        kc = col.counts[:, :n].cpu().numpy()
+        for e, m in enumerate(t.external_ids):
+            assert np.abs(kc[e] - np.array(counts[m])).max() <= 1, (step, m)
+        for m, f in fields.items():
+            g = lat.owned(m).cpu().numpy()
+            assert (np.abs(g - f) <= 1e-6 * np.abs(f) + 1e-12).all(), (step, m)

@@ -65,3 +65,34 @@ def test_c_stencil_bitwise():
             f = np.ascontiguousarray(z['f0_' + shape].copy())
             cpu.diffuse(f, 5.0 * min(dt, 0.01), olat.n_substeps(dt))
             assert np.array_equal(f, z['f_%s_dt%g' % (shape, dt)])
+
+
+@pytest.mark.parametrize('name', ['c2', 'c3kin', 'c5kin'])
+def test_c_oracle_dp45_vs_odeint_trajectories(name):
+    """The C oracle's DP45 (the GPU kernels' algorithm, rtol 1e-8) follows the
+    committed odeint trajectories (tests/golden/make_odeint_traj.py) within the
+    north-star 1e-6 relative + 1e-10 absolute, step after step; and the
+    seeded colony generator still reproduces the fixture's inputs."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import make_odeint_traj as mk
+    z = np.load(os.path.join(GOLDEN, '%s_odeint_traj.npz' % name))
+    (_, n_agents, stride, _, steps, every) = mk.CASES[name]
+    cfg, t, params, conc = mk._setup(name)
+    sample = z['sample']
+    assert np.array_equal(params[:, sample], z['params']) and np.array_equal(conc[:, sample], z['conc'])
+    p = np.ascontiguousarray(z['params'])
+    c = np.ascontiguousarray(z['conc'])
+    m2c = np.full(c.shape[1], float(z['m2c']))
+    h = np.zeros(c.shape[1])
+    desc = cpu.Desc(t)
+    k = 0
+    for step in range(1, steps + 1):
+        fl, _, st, _ = cpu.step_dopri5(desc, 1.0, p, c, m2c, h_state=h)
+        assert not st.any()
+        if step % every == 0:
+            ref = z['y'][:, k]
+            assert (np.abs(c[:t.n_dyn].T - ref) <= 1e-6 * np.abs(ref) + 1e-10).all(), step
+            fr = z['flux'][:, k]
+            assert (np.abs(fl.T - fr) <= 1e-6 * np.abs(fr) + 1e-10).all(), step
+            k += 1

@@ -168,7 +168,7 @@ def test_dopri5_matches_odeint(dev, name, variant):
 def test_dopri5_matches_c_oracle_all_agents(dev):
     cfg = configs.glc_lct_config()
     t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
-    n = 5000
+    n = 10_000                      # BASELINE config 2 size
     params, conc = configs.heterogeneous_colony(t, cfg, n)
     m2c = np.full(n, mmol_to_counts())
     eng = _engine(t, dev)
