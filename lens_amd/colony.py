@@ -90,6 +90,8 @@ class Colony:
         self.time = 0.0
         self.step_index = 0
         self.lattice: Optional[Lattice] = None
+        self.router = None       # distributed.AgentRouter (row-banded multi-rank lattice colonies)
+        self.ordinal = None      # global single-rank-order key (set by the router)
         self.location = None
         self.env_fields = None
         self.cells = cells
@@ -167,13 +169,30 @@ class Colony:
             put(self.location, location)
             self.refresh_bins()
 
+    def agent_array_names(self):
+        """Every per-agent array (agent = column), as attribute names: what
+        division gathers and the router migrates."""
+        names = ['params', 'conc', 'm2c', 'flux', 'counts', 'status', 'nsteps', 'h_state']
+        if self.location is not None:
+            names.append('location')
+        if self.cells is not None:
+            names += ['cell', 'divide', 'lin_root', 'lin_depth', 'lin_path']
+        if self.ordinal is not None:
+            names.append('ordinal')
+        return names
+
     def refresh_bins(self):
-        """Recompute bin sites and the agent-ordered bin occupancy (after moves)."""
+        """Recompute bin sites and the agent-ordered bin occupancy (after moves).
+        A row-banded colony with a router first moves agents that left this
+        rank's band to their owner (a collective: every rank calls it)."""
         lat = self.lattice
+        if self.router is not None:
+            self.router.route()
         lat.bin_sites(self.location, self.n, self.bin_lin, self.bin_ix)
         ix = self.bin_ix[:self.n]
         if self.n and (int(ix.min()) < lat.row_lo_global or int(ix.max()) >= lat.row_hi_global):
-            raise ValueError('agents outside this rank\'s row band: route them first')
+            raise ValueError('agents outside this rank\'s row band: attach a distributed.AgentRouter '
+                             '(division moves daughters across band edges)')
         self.occ = occupancy(self.bin_lin, self.n)
 
     def gather_external(self):
@@ -286,29 +305,44 @@ class Colony:
         """Growth process + TreeMass/DeriveGlobals, then division.  Returns the
         number of mothers that divided."""
         cm, n = self.cells, self.n
-        if n == 0:
+        if n == 0 and self.router is None:
             return 0
-        p = cm.vk_params(dt, self.step_index)
-        u = None
-        if cm.model == 'growth_protein' and cm.rng == 'stream':
-            u = torch.from_numpy(cm.host_uniforms(n)).to(self.device)
-        native.check(native._lib.vk_cell_step(
-            ctypes.byref(p), n, self.ld, native.ptr(self.cell), native.ptr(self.m2c), native.ptr(u),
-            native.ptr(self.lin_root), native.ptr(self.lin_depth), native.ptr(self.lin_path),
-            native.ptr(self.divide), native.stream_handle()), 'vk_cell_step')
         src = torch.empty(2 * n, dtype=torch.int32, device=self.device)
         kind = torch.empty(2 * n, dtype=torch.int32, device=self.device)
-        scratch = torch.empty(int(native._lib.vk_divide_scratch_bytes(n)), dtype=torch.uint8, device=self.device)
-        native.check(native._lib.vk_divide_plan(
-            native.ptr(self.divide), n, native.ptr(src), native.ptr(kind), native.ptr(self._n_out),
-            native.ptr(scratch), native.stream_handle()), 'vk_divide_plan')
-        n_out = int(self._n_out.item())
+        n_out = 0
+        if n:
+            p = cm.vk_params(dt, self.step_index)
+            u = None
+            if cm.model == 'growth_protein' and cm.rng == 'stream':
+                u = torch.from_numpy(cm.host_uniforms(n)).to(self.device)
+            native.check(native._lib.vk_cell_step(
+                ctypes.byref(p), n, self.ld, native.ptr(self.cell), native.ptr(self.m2c), native.ptr(u),
+                native.ptr(self.lin_root), native.ptr(self.lin_depth), native.ptr(self.lin_path),
+                native.ptr(self.divide), native.stream_handle()), 'vk_cell_step')
+            scratch = torch.empty(int(native._lib.vk_divide_scratch_bytes(n)), dtype=torch.uint8,
+                                  device=self.device)
+            native.check(native._lib.vk_divide_plan(
+                native.ptr(self.divide), n, native.ptr(src), native.ptr(kind), native.ptr(self._n_out),
+                native.ptr(scratch), native.stream_handle()), 'vk_divide_plan')
+            n_out = int(self._n_out.item())
+        if self.router is not None:
+            # collective every step: the global order of every rank's survivors
+            # and daughters (AgentRouter.division_ordinals); then, if any rank
+            # divided, daughters that left this band move to their owner
+            new_ord, n_div = self.router.division_ordinals(self.ordinal[:n], self.divide[:n] != 0, src, kind,
+                                                           n_out)
+            if n_out != n:
+                self._apply_division(n_out, src, kind, ordinal=new_ord)
+            elif n_div:
+                self.ordinal[:n] = new_ord
+                self.refresh_bins()
+            return n_out - n
         if n_out == n:
             return 0
         self._apply_division(n_out, src, kind)
         return n_out - n
 
-    def _apply_division(self, n_out, src, kind):
+    def _apply_division(self, n_out, src, kind, ordinal=None):
         ld_src = self.ld
         ld = max(self.ld, n_out)
         if n_out > self.ld:
@@ -353,6 +387,9 @@ class Colony:
                 native.ptr(cell), st), 'vk_divide_locations')
             self.location = loc
         self.cell, self.lin_root, self.lin_depth, self.lin_path = cell, root, depth, path
+        if ordinal is not None:
+            self.ordinal = torch.zeros(ld, dtype=torch.int64, device=dev)
+            self.ordinal[:n_out] = ordinal
         self.n, self.ld = n_out, ld
         if self.lattice is not None:
             self.bin_lin = torch.zeros(ld, dtype=torch.int32, device=dev)

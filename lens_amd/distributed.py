@@ -86,3 +86,178 @@ def make_uniform_allreduce(group=None):
             mm.copy_(t)
 
     return allreduce
+
+
+# ---------------------------------------------------------------------------
+# agent routing between row bands (division moves daughters across band edges)
+# ---------------------------------------------------------------------------
+
+class GlobalRoots:
+    """Root agent names for a multi-rank colony: ``str(global index)``, the
+    single-rank colony's default ids (Colony(agent_ids=None))."""
+
+    def __getitem__(self, i):
+        return str(int(i))
+
+    def __len__(self):          # pragma: no cover - informational
+        return 0
+
+
+class AgentRouter:
+    """Keeps every agent of a row-banded lattice colony on the rank that owns
+    its bin row, moving daughters that division placed past a
+    band edge (``daughter_locations``, vivarium/processes/multibody_physics.py:
+    77-87) with one ``all_to_all`` of packed agent rows.
+
+    Each agent also carries ``ordinal``: its position in the order a
+    single-rank colony would hold it in.  The reference's order -- survivors
+    in their order, then daughters in mother order, each mother's two
+    daughters in id order (vivarium/core/experiment.py:664-697) -- is
+    rank-count independent only through this global key: after a division
+    step a survivor's new ordinal is its old one minus the number of dividing
+    mothers (on ANY rank) before it, and daughter k of a mother with ordinal g
+    gets (survivors everywhere) + 2 * (dividing mothers before g) + k.  One
+    all-gather of the dividing mothers' ordinals per step provides that.  Each
+    rank keeps its agents sorted by ordinal, so the agent-ordered exchange
+    scatter adds a bin's agents in the single-rank order: a banded colony with
+    division equals the single-rank colony bit for bit.
+
+    ``agent_offset``: global index of this rank's first agent (the initial
+    colony is split by band in index order); root ids become global."""
+
+    def __init__(self, col, rank: int, world: int, group=None, agent_offset: int = None):
+        self.col, self.rank, self.world, self.group = col, rank, world, group
+        lat = col.lattice
+        bands = row_bands(lat.n_bins[0], world)
+        if (lat.row_lo_global, lat.row_hi_global) != bands[rank]:
+            raise ValueError('the lattice band %r is not rank %d of row_bands' % (
+                (lat.row_lo_global, lat.row_hi_global), rank))
+        dev = col.device
+        self.band_hi = torch.tensor([hi for _, hi in bands], dtype=torch.int64, device=dev)
+        self.staged = _host_staged(dev, group)
+        n = col.n
+        if agent_offset is None:
+            counts = self._all_gather_sizes(n)
+            agent_offset = int(sum(counts[:rank]))
+        col.ordinal = torch.zeros(col.ld, dtype=torch.int64, device=dev)
+        col.ordinal[:n] = torch.arange(agent_offset, agent_offset + n, device=dev)
+        if col.cells is not None:
+            col.lin_root[:n] = col.ordinal[:n].to(torch.int32)
+            col.roots = GlobalRoots()
+        col.router = self
+
+    # -- collectives (gloo stages device tensors through host memory) --------
+    def _dev(self, t):
+        return t.cpu() if self.staged else t
+
+    def _all_gather_sizes(self, k: int):
+        t = self._dev(torch.tensor([k], dtype=torch.int64, device=self.col.device))
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [int(x.item()) for x in out]
+
+    def _all_gather_var(self, t):
+        """Concatenation over ranks of a 1-D int64 tensor of any length."""
+        sizes = self._all_gather_sizes(t.numel())
+        m = max(sizes) if sizes else 0
+        if m == 0:
+            return torch.zeros(0, dtype=torch.int64, device=self.col.device)
+        pad = torch.zeros(m, dtype=torch.int64, device=self.col.device)
+        pad[:t.numel()] = t
+        pad = self._dev(pad)
+        out = [torch.zeros_like(pad) for _ in range(self.world)]
+        dist.all_gather(out, pad, group=self.group)
+        return torch.cat([o[:s] for o, s in zip(out, sizes)]).to(self.col.device)
+
+    # -- division ------------------------------------------------------------
+    def division_ordinals(self, old_ord, dividing, src, kind, n_out):
+        """(new ordinals of the n_out agents of this rank's division plan, the
+        number of mothers that divided on all ranks); src / kind from
+        vk_divide_plan.  A collective: every rank calls it every step."""
+        mothers = old_ord[dividing]
+        d_all = torch.sort(self._all_gather_var(mothers)).values
+        n_surv = sum(self._all_gather_sizes(int(old_ord.numel() - mothers.numel())))
+        a = src[:n_out].to(torch.int64)
+        kd = kind[:n_out].to(torch.int64)
+        g = old_ord[a]
+        before = torch.searchsorted(d_all, g)              # dividing mothers strictly before g
+        return torch.where(kd < 0, g - before, n_surv + 2 * before + kd), int(d_all.numel())
+
+    # -- migration -------------------------------------------------------------
+    def route(self):
+        """Send every agent whose bin row lies in another rank's band to that
+        rank; keep this rank's agents sorted by ordinal.  Collective."""
+        col, lat = self.col, self.col.lattice
+        n = col.n
+        lat.bin_sites(col.location, n, col.bin_lin, col.bin_ix)
+        dest = torch.bucketize(col.bin_ix[:n].to(torch.int64), self.band_hi, right=True)
+        leave = dest != self.rank
+        send_counts = torch.bincount(dest[leave], minlength=self.world)
+        order = torch.sort(dest[leave], stable=True).indices
+        idx_leave = torch.nonzero(leave).flatten()[order]
+        idx_stay = torch.nonzero(~leave).flatten()
+        names = col.agent_array_names()
+        send = self._pack(names, idx_leave)
+        send_counts_l = [int(x) for x in send_counts.tolist()]
+        sc = self._dev(send_counts.to(torch.int64))
+        rc = torch.zeros_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        recv_counts_l = [int(x) for x in rc.tolist()]
+        # every rank joins the payload exchange, even with nothing to move
+        # (skipping it locally would strand the ranks that do exchange)
+        width = send.shape[1]
+        recv = torch.zeros((sum(recv_counts_l), width), dtype=torch.float64,
+                           device='cpu' if self.staged else col.device)
+        dist.all_to_all_single(recv, self._dev(send), recv_counts_l, send_counts_l, group=self.group)
+        recv = recv.to(col.device)
+        if sum(send_counts_l) or sum(recv_counts_l):
+            self._rebuild(names, idx_stay, recv)
+        return sum(recv_counts_l)
+
+    def _pack(self, names, idx):
+        cols = []
+        for name in names:
+            t = getattr(self.col, name)
+            x = t.index_select(t.dim() - 1, idx)
+            x = x.reshape(1, -1) if t.dim() == 1 else x
+            if x.dtype == torch.float64:
+                pass
+            elif x.dtype == torch.int64:
+                x = x.contiguous().view(torch.float64)        # bits travel untouched
+            else:
+                x = x.to(torch.float64)                        # int32: exact
+            cols.append(x.t())
+        return torch.cat(cols, dim=1).contiguous() if cols else None
+
+    def _rebuild(self, names, idx_stay, recv):
+        col = self.col
+        n_new = idx_stay.numel() + recv.shape[0]
+        ld = col.ld if n_new <= col.ld else max(n_new, int(col.ld * 1.25) + 64)
+        # immigrants' ordinals: merge with the stayers by ordinal
+        off = 0
+        pieces = {}
+        for name in names:
+            t = getattr(col, name)
+            rows = 1 if t.dim() == 1 else t.shape[0]
+            r = recv[:, off:off + rows].t()
+            off += rows
+            if t.dtype == torch.int64:
+                r = r.contiguous().view(torch.int64)
+            elif t.dtype != torch.float64:
+                r = r.to(t.dtype)
+            stay = t.index_select(t.dim() - 1, idx_stay)
+            both = torch.cat([stay.reshape(rows, -1), r.reshape(rows, -1)], dim=1)
+            pieces[name] = both
+        perm = torch.sort(pieces['ordinal'].reshape(-1), stable=True).indices
+        for name in names:
+            t = getattr(col, name)
+            both = pieces[name].index_select(1, perm)
+            out = torch.zeros((ld,) if t.dim() == 1 else (t.shape[0], ld), dtype=t.dtype, device=col.device)
+            if t.dim() == 1:
+                out[:n_new] = both.reshape(-1)
+            else:
+                out[:, :n_new] = both
+            setattr(col, name, out)
+        col.n, col.ld = n_new, ld
+        col.bin_lin = torch.zeros(ld, dtype=torch.int32, device=col.device)
+        col.bin_ix = torch.zeros(ld, dtype=torch.int32, device=col.device)

@@ -137,3 +137,124 @@ def test_interior_band_without_halo_is_rejected():
         Lattice(['a'], (41, 23), (41.0, 23.0), 10.0, 5.0, device='cpu', row_band=(20, 25), halo=8)
     # the whole domain as one band needs no halo
     Lattice(['a'], (41, 23), (41.0, 23.0), 10.0, 5.0, device='cpu', row_band=(0, 41), halo=0)
+
+
+# ---------------------------------------------------------------------------
+# AgentRouter host logic (gloo, CPU tensors; the GPU colony version is in
+# tests/test_distributed_gpu.py)
+# ---------------------------------------------------------------------------
+
+class _FakeLattice:
+    def __init__(self, nx, band):
+        self.n_bins = [nx, 4]
+        self.row_lo_global, self.row_hi_global = band
+
+    def bin_sites(self, loc, n, bin_lin, ix):
+        ix[:n] = torch.floor(loc[0, :n]).to(torch.int32)
+        bin_lin[:n] = 0
+
+
+class _FakeColony:
+    """The per-agent arrays AgentRouter moves, in the Colony layout."""
+
+    def __init__(self, nx, band, xs, vals, ords, ld):
+        n = len(xs)
+        self.device = torch.device('cpu')
+        self.lattice = _FakeLattice(nx, band)
+        self.cells = None
+        self.n, self.ld = n, ld
+        self.location = torch.zeros((2, ld), dtype=torch.float64)
+        self.location[0, :n] = torch.tensor(xs, dtype=torch.float64)
+        self.params = torch.zeros((2, ld), dtype=torch.float64)
+        self.params[0, :n] = torch.tensor(vals, dtype=torch.float64)
+        self.params[1, :n] = -torch.tensor(vals, dtype=torch.float64)
+        self.counts = torch.zeros((1, ld), dtype=torch.int64)
+        self.counts[0, :n] = torch.tensor([int(v * 1e6) - (1 << 40) for v in vals], dtype=torch.int64)
+        self.status = torch.zeros(ld, dtype=torch.int32)
+        self.status[:n] = torch.tensor([int(v * 1000) for v in vals], dtype=torch.int32)
+        self.ordinal = torch.zeros(ld, dtype=torch.int64)
+        self.ordinal[:n] = torch.tensor(ords, dtype=torch.int64)
+        self.bin_lin = torch.zeros(ld, dtype=torch.int32)
+        self.bin_ix = torch.zeros(ld, dtype=torch.int32)
+
+    def agent_array_names(self):
+        return ['params', 'counts', 'status', 'location', 'ordinal']
+
+
+def _router_worker(rank, world, port, seed, q):
+    from lens_amd.distributed import AgentRouter
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        nx = 30
+        bands = row_bands(nx, world)
+        rng = np.random.default_rng(seed)
+        n_glob = 200
+        xs_all = rng.uniform(0, nx, n_glob)
+        owner = rng.integers(0, world, n_glob)          # agents start on arbitrary ranks
+        mine = np.flatnonzero(owner == rank)             # ordinal order = global index order
+        col = _FakeColony(nx, bands[rank], xs_all[mine].tolist(), (mine / 7.0 + 0.5).tolist(), mine.tolist(),
+                          ld=len(mine) + 3)
+        r = AgentRouter.__new__(AgentRouter)
+        r.col, r.rank, r.world, r.group, r.staged = col, rank, world, None, False
+        r.band_hi = torch.tensor([hi for _, hi in bands], dtype=torch.int64)
+        r.route()
+        n = col.n
+        got = {'ord': col.ordinal[:n].tolist(), 'x': col.location[0, :n].tolist(),
+               'p0': col.params[0, :n].tolist(), 'p1': col.params[1, :n].tolist(),
+               'counts': col.counts[0, :n].tolist(), 'status': col.status[:n].tolist()}
+        # division ordinals: a random dividing subset of the (now routed) agents
+        div = torch.tensor(rng.random(n_glob) < 0.3)[col.ordinal[:n]]
+        keep = torch.nonzero(~div).flatten()
+        moth = torch.nonzero(div).flatten()
+        src = torch.cat([keep, moth.repeat_interleave(2)]).to(torch.int32)
+        kind = torch.cat([torch.full((keep.numel(),), -1), torch.tensor([0, 1] * moth.numel())]).to(torch.int32)
+        new, n_div = r.division_ordinals(col.ordinal[:n], div, src, kind, src.numel())
+        got['new'] = new.tolist()
+        got['src_ord'] = col.ordinal[:n][src.to(torch.int64)].tolist()
+        got['kind'] = kind.tolist()
+        got['n_div'] = n_div
+        q.put((rank, bands[rank], got, xs_all.tolist(), (rng.random(0)).tolist()))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,seed', [(2, 1), (3, 2)])
+def test_agent_router_routes_and_orders(world, seed):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_router_worker, args=(r, world, port, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    xs_all = parts[0][3]
+    seen = []
+    for rank, band, got, _, _ in parts:
+        # every agent now lives in its band, sorted by ordinal, payload intact
+        assert all(band[0] <= int(np.floor(x)) < band[1] for x in got['x'])
+        assert got['ord'] == sorted(got['ord'])
+        for o, x, p0, p1, c, s in zip(got['ord'], got['x'], got['p0'], got['p1'], got['counts'], got['status']):
+            assert x == xs_all[o] and p0 == o / 7.0 + 0.5 and p1 == -p0
+            assert c == int(p0 * 1e6) - (1 << 40) and s == int(p0 * 1000)
+        seen += got['ord']
+    assert sorted(seen) == list(range(200))
+    # division ordinals == positions in the single-rank order (survivors, then daughters in mother order)
+    divided = sorted(o for _, _, got, _, _ in parts for o, k in zip(got['src_ord'], got['kind']) if k == 0)
+    survivors = sorted(set(range(200)) - set(divided))
+    want = {('s', o): i for i, o in enumerate(survivors)}
+    for i, o in enumerate(divided):
+        want[('d', o, 0)] = len(survivors) + 2 * i
+        want[('d', o, 1)] = len(survivors) + 2 * i + 1
+    allnew = []
+    for _, _, got, _, _ in parts:
+        assert got['n_div'] == len(divided)
+        for o, k, g in zip(got['src_ord'], got['kind'], got['new']):
+            assert g == want[('s', o) if k < 0 else ('d', o, k)]
+            allnew.append(g)
+    assert sorted(allnew) == list(range(len(survivors) + 2 * len(divided)))

@@ -1,0 +1,175 @@
+"""The real multi-rank lattice colony on one MI355X (needs a GPU).
+
+2 and 3 ranks (gloo; device buffers staged through host memory, as the
+driver's RCCL run does over xGMI) each own a row band of the lattice and the
+agents in it, and run the full ``Colony.step`` on cuda:0 through the HIP
+kernels: kinetics, one-step-lag gather, banded diffusion with k-deep halo
+exchange, agent-ordered exchange scatter, growth, derivers and division, and
+``AgentRouter`` migration of daughters placed past a band edge
+(``daughter_locations``, vivarium/processes/multibody_physics.py:77-87).
+After every step the assembled colony must equal the single-rank colony bit
+for bit: the same agents (phylogeny ids), in the same global order, with the
+same state, and the same fields.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+NX, NY, N, STEPS = 40, 32, 300, 30
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _colony_inputs():
+    """Global colony, in band-major order (the initial split keeps index order)."""
+    from lens_amd import configs
+    from lens_amd.rate_law_compiler import compile_rate_laws
+    cfg = configs.glc_ac_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    rng = np.random.default_rng(77)
+    x = rng.uniform(0.0, NX, N)
+    x[:60] = rng.uniform(NX / 2 - 1.0, NX / 2 + 1.0, 60)          # crowd the band edges
+    x[60:100] = rng.uniform(NX / 3 - 1.0, NX / 3 + 1.0, 40)
+    x[100:140] = rng.uniform(2 * NX / 3 - 1.0, 2 * NX / 3 + 1.0, 40)
+    loc = np.stack([x, rng.uniform(0.0, NY, N)])
+    order = np.argsort(np.floor(loc[0]), kind='stable')           # by bin row
+    loc = np.ascontiguousarray(loc[:, order])
+    params, conc = configs.heterogeneous_colony(t, cfg, N, seed=5)
+    mass = rng.uniform(1339.0, 2.4 * 1100.0, N)
+    angle = rng.uniform(0, 2 * np.pi, N)
+    return cfg, t, params, conc, loc, mass, angle
+
+
+def _make(dev, cfg, t, band, halo, params, conc, loc, mass, angle):
+    from lens_amd import configs, native
+    from lens_amd.cells import CellModel
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    lat = Lattice(['glc__D_e', 'ac_e'], (NX, NY), (float(NX), float(NY)), 10.0, 5.0, device=dev,
+                  row_band=band, halo=halo,
+                  initial={'glc__D_e': configs.gaussian_bump_field((NX, NY)), 'ac_e': np.zeros((NX, NY))})
+    cm = CellModel(model='growth', growth_rate=0.003, division_volume=2.4)
+    n = conc.shape[1]
+    col = Colony(cfg, n, device=dev, integrator='euler', environment=lat, table=t, cells=cm)
+    col.set_agents(params=params, conc=conc, location=loc)
+    col.set_cell_mass(mass)
+    rows = col.cell.cpu().numpy()
+    rows[native.VK_CELL_ANGLE, :n] = angle
+    col.cell.copy_(torch.from_numpy(rows))
+    col.gather_external()
+    return col, lat
+
+
+def _state(col, lat):
+    """{(root, depth, path): bytes of every per-agent array}, [(ordinal, key)],
+    the owned fields.  Root indices are global in both runs (the single-rank
+    colony's agents are the global colony in index order)."""
+    n = col.n
+    names = [a for a in col.agent_array_names() if a != 'ordinal']
+    arrays = {a: getattr(col, a)[..., :n].cpu().numpy() for a in names}
+    keys = list(zip(arrays['lin_root'].tolist(), arrays['lin_depth'].tolist(), arrays['lin_path'].tolist()))
+    per = {}
+    for j, key in enumerate(keys):
+        per[key] = {a: np.ascontiguousarray(v[..., j]).tobytes() for a, v in arrays.items()}
+    ords = col.ordinal[:n].cpu().numpy().tolist() if col.ordinal is not None else list(range(n))
+    return per, list(zip(ords, keys)), lat.owned().cpu().numpy().copy()
+
+
+def _worker(rank, world, port, halo, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from lens_amd.distributed import row_bands, make_halo_exchange, make_uniform_allreduce, AgentRouter
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        cfg, t, params, conc, loc, mass, angle = _colony_inputs()
+        band = row_bands(NX, world)[rank]
+        rows = np.floor(loc[0]).astype(int)
+        mine = np.flatnonzero((rows >= band[0]) & (rows < band[1]))
+        offset = int(mine[0]) if len(mine) else int(np.sum(rows < band[0]))
+        col, lat = _make(dev, cfg, t, band, halo, params[:, mine], conc[:, mine], loc[:, mine], mass[mine],
+                         angle[mine])
+        AgentRouter(col, rank, world, agent_offset=offset)
+        ex = make_halo_exchange(lat, rank, world)
+        ar = make_uniform_allreduce()
+        hist = []
+        for _ in range(STEPS):
+            col.step(1.0, halo_exchange=ex, allreduce=ar)
+            torch.cuda.synchronize()
+            hist.append(_state(col, lat))
+        col.check_status()
+        q.put((rank, band, hist))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,halo', [(2, 8), (3, 5)])
+def test_banded_colony_with_migration_equals_single_rank(world, halo):
+    import torch.multiprocessing as mp
+    from lens_amd.distributed import row_bands
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    cfg, t, params, conc, loc, mass, angle = _colony_inputs()
+    col, lat = _make(dev, cfg, t, None, 0, params, conc, loc, mass, angle)
+    ref = []
+    for _ in range(STEPS):
+        col.step(1.0)
+        torch.cuda.synchronize()
+        ref.append(_state(col, lat))
+    assert col.n > N + 20                    # the run divided
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, halo, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=150) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    bands = row_bands(NX, world)
+    moved = 0
+    for step in range(STEPS):
+        per_ref, ord_ref, f_ref = ref[step]
+        merged, ords, fields = {}, [], []
+        for rank, band, hist in parts:
+            per, ordr, f = hist[step]
+            assert not set(per) & set(merged)
+            merged.update(per)
+            ords += ordr
+            fields.append(f)
+        assert sorted(merged) == sorted(per_ref), step
+        # the global order: ordinals are the single-rank positions
+        ords.sort()
+        assert [o for o, _ in ords] == list(range(len(per_ref))), step
+        assert [aid for _, aid in ords] == [aid for _, aid in ord_ref], step
+        for aid, arrays in per_ref.items():
+            assert merged[aid] == arrays, (step, aid)
+        assert np.array_equal(np.concatenate(fields, axis=1), f_ref), step
+        # every agent sits in its rank's band (bin rows wrap: get_bin_site, lattice_utils.py:34-40)
+        for rank, band, hist in parts:
+            for aid in hist[step][0]:
+                x = np.frombuffer(hist[step][0][aid]['location'], dtype=np.float64)[0]
+                assert band[0] <= int(np.floor(x * NX / NX)) % NX < band[1]
+    # some daughters crossed a band edge: agents on a rank their root did not start on
+    for rank, band, hist in parts:
+        for root, depth, path in hist[-1][0]:
+            moved += not (band[0] <= np.floor(loc[0, root]) < band[1])
+    assert moved > 0
