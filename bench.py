@@ -224,11 +224,21 @@ def main():
         args.stencil_rows = 64 if world == 1 else 0
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
-    halo_ex = allred = None
+    halo_ex = allred = balancer = None
     if world > 1 and lat is not None:
         from lens_amd.distributed import make_halo_exchange, make_uniform_allreduce
         halo_ex = make_halo_exchange(lat, rank, world)
         allred = make_uniform_allreduce()
+    elif world > 1 and col.cells is not None:
+        # agent-sharded C5: divisions are rank-local; even the shards out when
+        # they drift more than 5 % apart (one all_to_all)
+        from lens_amd.distributed import AgentBalancer
+        balancer = AgentBalancer(col, rank, world, tolerance=0.05)
+
+    def one_step(timing):
+        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing)
+        if balancer is not None:
+            balancer.balance()
 
     def barrier():
         if dist is not None:
@@ -242,7 +252,7 @@ def main():
     col.count_attempts(True)
     # warmup runs exactly the timed loop body (first-use costs land here)
     for k in range(args.warmup):
-        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=warm_timing[k])
+        one_step(warm_timing[k])
     barrier()
     col.check_status()
     col.attempts.zero_()
@@ -252,7 +262,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         agent_steps += col.n
-        col.step(1.0, halo_exchange=halo_ex, allreduce=allred, timing=timing[k])
+        one_step(timing[k])
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()

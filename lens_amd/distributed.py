@@ -197,7 +197,7 @@ class AgentRouter:
         idx_leave = torch.nonzero(leave).flatten()[order]
         idx_stay = torch.nonzero(~leave).flatten()
         names = col.agent_array_names()
-        send = self._pack(names, idx_leave)
+        send = pack_agents(col, names, idx_leave)
         send_counts_l = [int(x) for x in send_counts.tolist()]
         sc = self._dev(send_counts.to(torch.int64))
         rc = torch.zeros_like(sc)
@@ -211,53 +211,127 @@ class AgentRouter:
         dist.all_to_all_single(recv, self._dev(send), recv_counts_l, send_counts_l, group=self.group)
         recv = recv.to(col.device)
         if sum(send_counts_l) or sum(recv_counts_l):
-            self._rebuild(names, idx_stay, recv)
+            stay = {name: take_agents(col, name, idx_stay) for name in names}
+            both = {name: torch.cat([stay[name], piece], dim=1)
+                    for name, piece in unpack_agents(col, names, recv).items()}
+            # immigrants merge with the stayers by ordinal
+            perm = torch.sort(both['ordinal'].reshape(-1), stable=True).indices
+            install_agents(col, names, {name: v.index_select(1, perm) for name, v in both.items()})
+            col.bin_lin = torch.zeros(col.ld, dtype=torch.int32, device=col.device)
+            col.bin_ix = torch.zeros(col.ld, dtype=torch.int32, device=col.device)
         return sum(recv_counts_l)
 
-    def _pack(self, names, idx):
-        cols = []
-        for name in names:
-            t = getattr(self.col, name)
-            x = t.index_select(t.dim() - 1, idx)
-            x = x.reshape(1, -1) if t.dim() == 1 else x
-            if x.dtype == torch.float64:
-                pass
-            elif x.dtype == torch.int64:
-                x = x.contiguous().view(torch.float64)        # bits travel untouched
-            else:
-                x = x.to(torch.float64)                        # int32: exact
-            cols.append(x.t())
-        return torch.cat(cols, dim=1).contiguous() if cols else None
 
-    def _rebuild(self, names, idx_stay, recv):
+# ---------------------------------------------------------------------------
+# packing per-agent SoA columns into rows of float64 (one all_to_all payload)
+# ---------------------------------------------------------------------------
+
+def take_agents(col, name, idx):
+    """Columns ``idx`` of the per-agent array ``name`` as a [rows, k] tensor."""
+    t = getattr(col, name)
+    x = t.index_select(t.dim() - 1, idx)
+    return x.reshape(1, -1) if t.dim() == 1 else x
+
+
+def pack_agents(col, names, idx):
+    """[k, width] float64: one row per agent; int64 columns travel as raw bits,
+    int32 columns as exact float64 values."""
+    cols = []
+    for name in names:
+        x = take_agents(col, name, idx)
+        if x.dtype == torch.int64:
+            x = x.contiguous().view(torch.float64)
+        elif x.dtype != torch.float64:
+            x = x.to(torch.float64)
+        cols.append(x.t())
+    return torch.cat(cols, dim=1).contiguous()
+
+
+def unpack_agents(col, names, recv):
+    """Inverse of :func:`pack_agents`: {name: [rows, k] tensor of the array's dtype}."""
+    out, off = {}, 0
+    for name in names:
+        t = getattr(col, name)
+        rows = 1 if t.dim() == 1 else t.shape[0]
+        r = recv[:, off:off + rows].t().contiguous()
+        off += rows
+        if t.dtype == torch.int64:
+            r = r.view(torch.int64)
+        elif t.dtype != torch.float64:
+            r = r.to(t.dtype)
+        out[name] = r
+    return out
+
+
+def install_agents(col, names, pieces):
+    """Replace every per-agent array by ``pieces[name]`` ([rows, n_new]),
+    growing the capacity when needed."""
+    n_new = pieces[names[0]].shape[1]
+    ld = col.ld if n_new <= col.ld else max(n_new, int(col.ld * 1.25) + 64)
+    for name in names:
+        t = getattr(col, name)
+        out = torch.zeros((ld,) if t.dim() == 1 else (t.shape[0], ld), dtype=t.dtype, device=col.device)
+        if t.dim() == 1:
+            out[:n_new] = pieces[name].reshape(-1)
+        else:
+            out[:, :n_new] = pieces[name]
+        setattr(col, name, out)
+    col.n, col.ld = n_new, ld
+
+
+class AgentBalancer:
+    """Agent-sharded colonies without a lattice (BASELINE configs 2 and 5):
+    division is rank-local, so ranks drift apart in agent count; when the
+    largest rank holds more than (1 + tolerance) x the mean, agents move
+    between neighbouring ranks so that every rank holds a near-equal
+    contiguous slice of the concatenated (rank-major) order -- one all_to_all
+    of packed agent rows, order preserved (alltoallv after
+    division imbalance).  Agents without a lattice are independent, so
+    placement changes no result; ``agent_ids`` stay global (GlobalRoots)."""
+
+    def __init__(self, col, rank: int, world: int, group=None, tolerance: float = 0.05,
+                 agent_offset: int = None):
+        if col.lattice is not None:
+            raise ValueError('lattice colonies are placed by band: use AgentRouter')
+        self.col, self.rank, self.world, self.group, self.tolerance = col, rank, world, group, tolerance
+        self.staged = _host_staged(col.device, group)
+        if col.cells is not None:
+            if agent_offset is None:
+                agent_offset = int(sum(self._sizes(col.n)[:rank]))
+            col.lin_root[:col.n] = torch.arange(agent_offset, agent_offset + col.n, device=col.device,
+                                                dtype=torch.int32)
+            col.roots = GlobalRoots()
+        self.moves = 0
+
+    def _sizes(self, k):
+        t = torch.tensor([k], dtype=torch.int64)
+        t = t if self.staged or self.col.device.type == 'cpu' else t.to(self.col.device)
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t, group=self.group)
+        return [int(x.item()) for x in out]
+
+    def balance(self, force: bool = False) -> int:
+        """Collective.  Returns the number of agents this rank received."""
         col = self.col
-        n_new = idx_stay.numel() + recv.shape[0]
-        ld = col.ld if n_new <= col.ld else max(n_new, int(col.ld * 1.25) + 64)
-        # immigrants' ordinals: merge with the stayers by ordinal
-        off = 0
-        pieces = {}
-        for name in names:
-            t = getattr(col, name)
-            rows = 1 if t.dim() == 1 else t.shape[0]
-            r = recv[:, off:off + rows].t()
-            off += rows
-            if t.dtype == torch.int64:
-                r = r.contiguous().view(torch.int64)
-            elif t.dtype != torch.float64:
-                r = r.to(t.dtype)
-            stay = t.index_select(t.dim() - 1, idx_stay)
-            both = torch.cat([stay.reshape(rows, -1), r.reshape(rows, -1)], dim=1)
-            pieces[name] = both
-        perm = torch.sort(pieces['ordinal'].reshape(-1), stable=True).indices
-        for name in names:
-            t = getattr(col, name)
-            both = pieces[name].index_select(1, perm)
-            out = torch.zeros((ld,) if t.dim() == 1 else (t.shape[0], ld), dtype=t.dtype, device=col.device)
-            if t.dim() == 1:
-                out[:n_new] = both.reshape(-1)
-            else:
-                out[:, :n_new] = both
-            setattr(col, name, out)
-        col.n, col.ld = n_new, ld
-        col.bin_lin = torch.zeros(ld, dtype=torch.int32, device=col.device)
-        col.bin_ix = torch.zeros(ld, dtype=torch.int32, device=col.device)
+        sizes = self._sizes(col.n)
+        total = sum(sizes)
+        if total == 0 or (not force and max(sizes) <= (1 + self.tolerance) * total / self.world):
+            return 0
+        start = sum(sizes[:self.rank])
+        bounds = [total * r // self.world for r in range(self.world + 1)]    # target slices
+        g = torch.arange(start, start + col.n, device=col.device)
+        dest = torch.bucketize(g, torch.tensor(bounds[1:], device=col.device), right=True)
+        send_counts = torch.bincount(dest, minlength=self.world)
+        names = col.agent_array_names()
+        send = pack_agents(col, names, torch.arange(col.n, device=col.device))   # dest is monotone
+        send_l = [int(x) for x in send_counts.tolist()]
+        recv_l = [max(0, min(sizes_hi, bounds[self.rank + 1]) - max(sizes_lo, bounds[self.rank]))
+                  for sizes_lo, sizes_hi in [(sum(sizes[:r]), sum(sizes[:r + 1])) for r in range(self.world)]]
+        recv = torch.zeros((sum(recv_l), send.shape[1]), dtype=torch.float64,
+                           device='cpu' if self.staged else col.device)
+        dist.all_to_all_single(recv, send.cpu() if self.staged else send, recv_l, send_l, group=self.group)
+        install_agents(col, names, unpack_agents(col, names, recv.to(col.device)))
+        got = sum(recv_l) - send_l[self.rank]
+        self.moves += got
+        return got
+

@@ -258,3 +258,44 @@ def test_agent_router_routes_and_orders(world, seed):
             assert g == want[('s', o) if k < 0 else ('d', o, k)]
             allnew.append(g)
     assert sorted(allnew) == list(range(len(survivors) + 2 * len(divided)))
+
+
+def _balance_worker(rank, world, port, sizes, q):
+    from lens_amd.distributed import AgentBalancer
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        start = sum(sizes[:rank])
+        g = list(range(start, start + sizes[rank]))
+        col = _FakeColony(30, (0, 30), [0.5] * len(g), [x / 3.0 for x in g], g, ld=len(g) + 1)
+        col.lattice = None
+        b = AgentBalancer(col, rank, world, tolerance=0.05)
+        got = b.balance()
+        n = col.n
+        q.put((rank, col.ordinal[:n].tolist(), col.params[0, :n].tolist(), col.counts[0, :n].tolist(), got))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('sizes', [(10, 50), (40, 3, 17), (0, 12, 30, 1)])
+def test_agent_balancer_evens_out_in_order(sizes):
+    world = len(sizes)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balance_worker, args=(r, world, port, list(sizes), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    total = sum(sizes)
+    glob = [o for _, ords, _, _, _ in parts for o in ords]
+    assert glob == list(range(total))                     # rank-major order preserved
+    for r, ords, p0, counts, _ in parts:
+        assert len(ords) == (r + 1) * total // world - r * total // world
+        assert p0 == [o / 3.0 for o in ords]
+        assert counts == [int(o / 3.0 * 1e6) - (1 << 40) for o in ords]

@@ -173,3 +173,106 @@ def test_banded_colony_with_migration_equals_single_rank(world, halo):
         for root, depth, path in hist[-1][0]:
             moved += not (band[0] <= np.floor(loc[0, root]) < band[1])
     assert moved > 0
+
+
+# ---------------------------------------------------------------------------
+# C5-style agent sharding without a lattice: rank-local division + rebalancing
+# ---------------------------------------------------------------------------
+
+N5, STEPS5 = 600, 20
+
+
+def _c5_inputs():
+    from lens_amd import configs
+    from lens_amd.rate_law_compiler import compile_rate_laws
+    cfg = configs.synthetic_network(n_species=50, n_reactions=40, n_enzymes=10)
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    params, conc = configs.heterogeneous_colony(t, cfg, N5, seed=9, sigma=0.2)
+    rng = np.random.default_rng(10)
+    mass = rng.uniform(1339.0, 2.4 * 1100.0, N5)
+    mass[:N5 // 3] = rng.uniform(2.3 * 1100.0, 2.4 * 1100.0, N5 // 3)     # rank 0 divides first
+    return cfg, t, params, conc, mass
+
+
+def _c5_colony(dev, cfg, t, params, conc, mass):
+    from lens_amd.cells import CellModel
+    from lens_amd.colony import Colony
+    cm = CellModel(model='growth', growth_rate=0.003, division_volume=2.4)
+    n = conc.shape[1]
+    col = Colony(cfg, n, device=dev, integrator='dopri5', environment='held', table=t, cells=cm,
+                 capacity=n + 64)
+    col.set_agents(params=params, conc=conc)
+    col.set_cell_mass(mass)
+    return col
+
+
+def _c5_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from lens_amd.distributed import AgentBalancer
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        cfg, t, params, conc, mass = _c5_inputs()
+        lo, hi = N5 * rank // world, N5 * (rank + 1) // world
+        col = _c5_colony(dev, cfg, t, params[:, lo:hi], conc[:, lo:hi], mass[lo:hi])
+        bal = AgentBalancer(col, rank, world, tolerance=0.02, agent_offset=lo)
+        sizes = []
+        for _ in range(STEPS5):
+            col.step(1.0)
+            sizes.append(col.n)
+            bal.balance()
+        col.check_status()
+        torch.cuda.synchronize()
+        q.put((rank, _state_held(col), sizes, bal.moves))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _state_held(col):
+    n = col.n
+    arrays = {a: getattr(col, a)[..., :n].cpu().numpy() for a in col.agent_array_names()}
+    keys = list(zip(arrays['lin_root'].tolist(), arrays['lin_depth'].tolist(), arrays['lin_path'].tolist()))
+    return [(k, {a: np.ascontiguousarray(v[..., j]).tobytes() for a, v in arrays.items()})
+            for j, k in enumerate(keys)]
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_sharded_c5_with_rebalancing_equals_single_rank(world):
+    """Agent-per-wavefront DP45 on the C5 network + growth/division, agents
+    sharded over ranks and rebalanced after divisions: every agent's state
+    equals the single-rank colony's bit for bit (without a lattice agents are
+    independent, so their placement -- and the order of the concatenated
+    ranks -- changes no result)."""
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    cfg, t, params, conc, mass = _c5_inputs()
+    col = _c5_colony(dev, cfg, t, params, conc, mass)
+    for _ in range(STEPS5):
+        col.step(1.0)
+    col.check_status()
+    ref = _state_held(col)
+    assert col.n > N5 + 50
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c5_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=150) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    merged = dict(item for _, st, _, _ in parts for item in st)
+    assert len(merged) == sum(len(st) for _, st, _, _ in parts)
+    assert sorted(merged) == sorted(k for k, _ in ref)
+    for k, b in ref:
+        assert merged[k] == b, k
+    assert sum(m for _, _, _, m in parts) > 0                  # rebalancing moved agents
+    final = [len(st) for _, st, _, _ in parts]
+    assert max(final) <= 1.02 * sum(final) / world + 1          # within the balancer's tolerance
