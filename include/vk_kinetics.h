@@ -183,6 +183,17 @@ int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
                const double *uniform, vk_stream_t stream);
 
+/* As vk_diffuse for a call that ends at the last substep, except that the
+ * last substep writes delta = new - field into `delta` (same layout; zero on
+ * uniform planes) and leaves `field` as it was: DiffusionField.next_update's
+ * delta (diffusion_field.py:385-394), for an accumulate updater that applies
+ * it later (multi-rate schedules, lens_amd.process.BatchedDiffusionField).  */
+int vk_diffuse_delta(double *field, double *work0, double *work1, double *delta, int32_t n_fields,
+                     int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
+                     int32_t hi_max, int32_t edge_top, int32_t edge_bot, int32_t sub_begin,
+                     int32_t sub_count, int32_t n_sub, double coeff_dt, const double *uniform,
+                     vk_stream_t stream);
+
 /* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
  * 1..15; 1 = one launch per substep; default 9).  Each call is planned as the
  * fewest odd-depth passes <= k, as even as possible.  Returns the previous

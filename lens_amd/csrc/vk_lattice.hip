@@ -36,9 +36,8 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
                                                            const double *f0,
                                                            int64_t field_stride, int ny, int lo, int hi,
                                                            int top_reflect, int bot_reflect, double coef,
-                                                           const double *__restrict__ uniform) {
+                                                           const double *__restrict__ uniform, int delta_mode) {
     const int f = blockIdx.z;
-    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform: delta is zero
     const int j = blockIdx.x * ST_BX + threadIdx.x;
     const int r0 = lo + blockIdx.y * ST_RB;
     if (j >= ny || r0 >= hi) return;
@@ -46,6 +45,11 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
     const double *s = src + (int64_t)f * field_stride;
     double *d = dst + (int64_t)f * field_stride;
     const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
+    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) {   // uniform plane: the delta is zero
+        if (delta_mode)
+            for (int r = r0; r < r1; ++r) d[(int64_t)r * ny + j] = 0.0;
+        return;
+    }
     const int jl = j > 0 ? j - 1 : 0;
     const int jr = j < ny - 1 ? j + 1 : ny - 1;
     const int ru = (r0 == top_reflect) ? r0 : r0 - 1;
@@ -59,8 +63,10 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
         const double lap = (((up + left) + (-4.0 * c)) + right) + down;
         double v = c + coef * lap;
         if (g) {
+            // delta_mode: the reference's delta = field_new - field, applied
+            // later by the accumulate updater (diffusion_field.py:394)
             const double base = g[(int64_t)r * ny + j];
-            v = base + (v - base);
+            v = delta_mode ? v - base : base + (v - base);
         }
         d[(int64_t)r * ny + j] = v;
         up = c;
@@ -151,7 +157,7 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         if (k == 1) {
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
-                               hi, top_reflect, bot_reflect, coeff_dt, uniform);
+                               hi, top_reflect, bot_reflect, coeff_dt, uniform, 0);
         } else if (g_stencil_kernel >= 6 && (k == 7 || k == 9 || k == 11)) {
             (g_stencil_kernel == 6 ? vk_launch_wl6nt : vk_launch_wl6ntl)(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
                             bot_reflect, coeff_dt, uniform);
@@ -185,6 +191,34 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         j += k;
     }
     return VK_OK;
+}
+
+extern "C" int vk_diffuse_delta(double *field, double *work0, double *work1, double *delta, int32_t n_fields,
+                                int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
+                                int32_t hi_max, int32_t edge_top, int32_t edge_bot, int32_t sub_begin,
+                                int32_t sub_count, int32_t n_sub, double coeff_dt, const double *uniform,
+                                vk_stream_t stream) {
+    if (!delta || sub_count < 1 || sub_begin + sub_count != n_sub) {
+        vk::set_error("vk_diffuse_delta: needs a delta buffer and the call must end at the last substep");
+        return VK_ERR_ARG;
+    }
+    // substeps before the last: the ordinary passes, none of them final (n_sub + 1),
+    // over one more row on each side (the last substep's neighbours) where there is one
+    if (sub_count > 1) {
+        const int rc = vk_diffuse(field, work0, work1, n_fields, field_stride, ny, std::max(lo_min, row_lo - 1),
+                                  std::min(hi_max, row_hi + 1), lo_min, hi_max, edge_top, edge_bot, sub_begin,
+                                  sub_count - 1, n_sub + 1, coeff_dt, uniform, stream);
+        if (rc) return rc;
+    }
+    const int jl = n_sub - 1;
+    double *work[2] = {work0, work1};
+    const double *src = jl == 0 ? field : work[(jl - 1) & 1];
+    const int top_reflect = edge_top ? lo_min : -1;
+    const int bot_reflect = edge_bot ? hi_max - 1 : 0x7fffffff;
+    dim3 grid((ny + ST_BX - 1) / ST_BX, (row_hi - row_lo + ST_RB - 1) / ST_RB, n_fields);
+    hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, (hipStream_t)stream, src, delta, field, field_stride,
+                       ny, row_lo, row_hi, top_reflect, bot_reflect, coeff_dt, uniform, 1);
+    return vk::launch_check("vk_diffuse_delta");
 }
 
 // ---------------------------------------------------------------------------

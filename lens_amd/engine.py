@@ -1,0 +1,265 @@
+"""Experiment-shaped driver: the reference's multi-rate update loop, batched.
+
+``Experiment`` restates vivarium.core.experiment.Experiment (experiment.py:
+1181-1450) over a nested-dict store, with the same scheduling semantics:
+
+* processes are visited depth first (the order of the nested ``processes``
+  dict); a process runs when its front time <= time, with timestep =
+  min(front + local_timestep, interval) - front, and computes its update
+  from the state at that moment (InvokeProcess / ``config['invoke']``,
+  :1157-1178, 1282-1311);
+* the global step is the smallest timestep that ran; the updates whose
+  front lands by then are applied in front order (:1395-1435); the derivers
+  run after every applied step and once at construction (:1247, 1319-1349);
+* value updates follow Store.apply_update (:586-739): branches recurse,
+  leaves apply the schema updater (accumulate by default) or an inline
+  ``{'_value', '_updater'}`` one; ``update_field_with_exchange`` gets the
+  agent's ``global`` / ``dimensions`` states through its port_mapping
+  (registry.py:149-183).
+
+What is batched (SURVEY.md §8 a9 + N2):
+
+* ``config['invoke'] = BatchedInvoke()`` turns every agent's
+  ``BatchedConvenienceKinetics.next_update`` of a step into one kernel
+  launch (lens_amd/invoke.py);
+* ``update_field_with_exchange`` on a device field (a torch CUDA tensor, as
+  :class:`lens_amd.process.BatchedDiffusionField` keeps them) never runs per
+  agent: the counts are queued while a step's updates are applied and
+  scattered by one agent-ordered launch (``vk_exchange_sorted``) before any
+  other update touches that field and before the derivers -- the same
+  additions in the same order, so the field is bit-identical to the
+  reference's one-agent-at-a-time updater.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+INFINITY = float('inf')
+N_A_LEGACY = 6.022140857e23
+
+
+def normalize_path(path) -> Tuple:
+    """experiment.py:1123-1130 ('..' steps up)."""
+    progress = []
+    for step in path:
+        if step == '..' and progress:
+            progress = progress[:-1]
+        else:
+            progress.append(step)
+    return tuple(progress)
+
+
+def _accumulate(current, new, states):
+    return current + new
+
+
+def _set(current, new, states):
+    return new
+
+
+def _bin_site(location, n_bins, bounds):
+    """lattice_utils.py:34-40."""
+    i = int(np.floor(location[0] * n_bins[0] / bounds[0])) % n_bins[0]
+    j = int(np.floor(location[1] * n_bins[1] / bounds[1])) % n_bins[1]
+    return i, j
+
+
+class _InvokeNow:
+    def __init__(self, process, interval, states):
+        self.update = process.next_update(interval, states)
+
+    def get(self, timeout=0):
+        return self.update
+
+
+class Experiment:
+    def __init__(self, config):
+        self.processes = config['processes']
+        self.topology = config['topology']
+        self.invoke = config.get('invoke') or _InvokeNow
+        self.avogadro = config.get('avogadro', N_A_LEGACY)
+        self.state = _copy_tree(config.get('initial_state', {}))
+        self.schema: Dict[Tuple, str] = {}
+        self.updaters = {'accumulate': _accumulate, 'set': _set,
+                         'update_field_with_exchange': self._update_field_with_exchange}
+        self._exchange: Dict[Tuple, list] = {}      # device field path -> queued (location, dims, count)
+        self.local_time = 0.0
+        for path, proc in self._walk(self.processes, ()):
+            for port, port_schema in proc.ports_schema().items():
+                self._register(self.port_path(path, port), port_schema)
+        self.send_updates([])
+
+    # -- store -------------------------------------------------------------------
+    def _walk(self, node, path):
+        out = []
+        for key, value in node.items():
+            if isinstance(value, dict):
+                out += self._walk(value, path + (key,))
+            else:
+                out.append((path + (key,), value))
+        return out
+
+    def _topology_of(self, path):
+        t = self.topology
+        for key in path:
+            t = t[key]
+        return t
+
+    def port_path(self, proc_path, port):
+        return normalize_path(proc_path[:-1] + tuple(self._topology_of(proc_path)[port]))
+
+    def get(self, path):
+        v = self.state
+        for key in path:
+            v = v[key]
+        return v
+
+    def _register(self, path, schema):
+        if not isinstance(schema, dict):
+            return
+        keys = [k for k in schema if not k.startswith('_')]
+        if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
+            if '_updater' in schema:           # a schema without one keeps the store's updater
+                self.schema.setdefault(path, schema['_updater'])
+            if '*' not in path:
+                node = self.state
+                for key in path[:-1]:
+                    node = node.setdefault(key, {})
+                if path[-1] not in node:
+                    node[path[-1]] = schema.get('_value', schema.get('_default'))
+            return
+        for k in keys:
+            self._register(path + (k,), schema[k])
+
+    def _updater_at(self, path):
+        if path in self.schema:
+            return self.schema[path]
+        for pat, name in self.schema.items():
+            if len(pat) == len(path) and all(p == '*' or p == q for p, q in zip(pat, path)):
+                return name
+        return 'accumulate'
+
+    # -- updates ---------------------------------------------------------------
+    def process_states(self, path, proc):
+        return {port: self.get(self.port_path(path, port)) for port in proc.ports_schema()}
+
+    def apply_update(self, update, proc_path):
+        for port, value in update.items():
+            self._apply(self.port_path(proc_path, port), value, proc_path)
+
+    def _apply(self, path, update, proc_path):
+        parent = self.get(path[:-1])
+        if path[-1] not in parent:
+            return
+        current = parent[path[-1]]
+        inline = isinstance(update, dict) and '_updater' in update
+        if isinstance(current, dict) and not inline:
+            for key, value in update.items():
+                self._apply(path + (key,), value, proc_path)
+            return
+        states = None
+        if inline:
+            spec = update['_updater']
+            name, mapping = (spec, None) if isinstance(spec, str) else (spec['updater'], spec.get('port_mapping'))
+            value = update.get('_value')
+            if mapping is not None:
+                states = {up: self.get(self.port_path(proc_path, pp)) for up, pp in mapping.items()}
+        else:
+            name, value = self._updater_at(path), update
+        if name != 'update_field_with_exchange':
+            self._flush(path)                        # queued exchange lands first
+        parent[path[-1]] = self.updaters[name](current, value, states, path) \
+            if name == 'update_field_with_exchange' else self.updaters[name](current, value, states)
+
+    def _update_field_with_exchange(self, current, count, states, path):
+        loc = states['global']['location']
+        dims = states['dimensions']
+        if _is_device(current):
+            self._exchange.setdefault(path, []).append((loc, dims, int(count)))
+            return current
+        delta = np.zeros((dims['n_bins'][0], dims['n_bins'][1]), dtype=np.float64)
+        i, j = _bin_site(loc, dims['n_bins'], dims['bounds'])
+        binvol = (dims['depth'] * dims['bounds'][0] * dims['bounds'][1]) * 1e-15 / (dims['n_bins'][0] * dims['n_bins'][1])
+        delta[i, j] += count / (binvol * self.avogadro) * 1000.0
+        return current + delta
+
+    def _flush(self, path=None):
+        """Scatter the queued exchange counts of one device field (or all) in agent order."""
+        paths = [path] if path is not None else list(self._exchange)
+        for p in paths:
+            queued = self._exchange.pop(p, None)
+            if not queued:
+                continue
+            from lens_amd.process import scatter_exchange
+            parent = self.get(p[:-1])
+            parent[p[-1]] = scatter_exchange(parent[p[-1]], queued, self.avogadro)
+
+    def send_updates(self, updates, derivers=None):
+        for update, path in updates:
+            self.apply_update(update.get(), path)
+        self._flush()
+        if derivers is None:
+            derivers = [(p, s) for p, s in self._walk(self.processes, ()) if s.is_deriver()]
+        for path, deriver in derivers:
+            self.apply_update(deriver.next_update(0, self.process_states(path, deriver)), path)
+            self._flush()
+
+    # -- Experiment.update (experiment.py:1351-1450) ---------------------------------
+    def update(self, interval):
+        time = 0
+        front = {}
+        while time < interval:
+            full_step = INFINITY
+            everything = self._walk(self.processes, ())
+            processes = [(p, s) for p, s in everything if not s.is_deriver()]
+            derivers = [(p, s) for p, s in everything if s.is_deriver()]
+            paths = {p for p, _ in processes}
+            front = {p: f for p, f in front.items() if p in paths}
+            for path, proc in processes:
+                if path not in front:
+                    front[path] = {'time': time, 'update': None}
+                process_time = front[path]['time']
+                if process_time <= time:
+                    future = min(process_time + proc.local_timestep(), interval)
+                    timestep = future - process_time
+                    pending = self.invoke(proc, timestep, self.process_states(path, proc))
+                    if timestep < full_step:
+                        full_step = timestep
+                    front[path]['time'] = future
+                    front[path]['update'] = (pending, path)
+            if full_step == INFINITY:
+                next_event = interval
+                for _ in front.keys():
+                    if front[path]['time'] < next_event:   # the reference's stale `path` (:1414-1419)
+                        next_event = front[path]['time']
+                time = next_event
+            else:
+                future = time + full_step
+                updates = []
+                for path, advance in front.items():
+                    if advance['time'] <= future and advance['update'] is not None:
+                        updates.append(advance['update'])
+                        advance['update'] = None
+                self.send_updates(updates, derivers)
+                time = future
+                self.local_time += full_step
+        return self
+
+
+def _is_device(x) -> bool:
+    return getattr(x, 'is_cuda', False)
+
+
+def _copy_tree(t):
+    if isinstance(t, dict):
+        return {k: _copy_tree(v) for k, v in t.items()}
+    if isinstance(t, np.ndarray):
+        return t.copy()
+    if _is_device(t):
+        return t.clone()
+    if isinstance(t, list):
+        return list(t)
+    return t

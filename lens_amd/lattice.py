@@ -51,6 +51,7 @@ class Lattice:
     def __init__(self, molecules: Sequence[str], n_bins, bounds, depth: float, diffusion: float,
                  device=None, row_band=None, halo: int = 0, avogadro: float = N_A_LEGACY,
                  initial=None):
+        native.load()            # no CPU fallback: the kernels or an error
         self.molecules = list(molecules)
         self.n_bins = [int(n_bins[0]), int(n_bins[1])]
         self.bounds = [float(bounds[0]), float(bounds[1])]
@@ -187,6 +188,25 @@ class Lattice:
         if events is not None:
             events[1].record()
         return n_sub
+
+    def diffuse_delta(self, timestep: float, delta=None, allreduce=None):
+        """DiffusionField.next_update's field delta (diffusion_field.py:385-407):
+        ``delta = new - field`` for every plane (zero for uniform planes), with
+        ``fields`` left as they were -- an accumulate updater applies it later
+        (vk_diffuse_delta).  Single-domain lattices only."""
+        if self.pad_top or self.pad_bot:
+            raise ValueError('diffuse_delta: a row band with halo rows is not supported')
+        n_sub = n_substeps(timestep, self.diffusion_dt)
+        coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
+        mm = self.uniform_summary(allreduce)
+        if delta is None:
+            delta = torch.empty_like(self.fields)
+        native.check(native._lib.vk_diffuse_delta(
+            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1), native.ptr(delta),
+            len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, self.row_lo, self.row_hi,
+            int(self.edge_top), int(self.edge_bot), 0, n_sub, n_sub, coeff_dt, native.ptr(mm),
+            native.stream_handle()), 'vk_diffuse_delta')
+        return delta
 
     def state_buffer(self, j: int):
         """Buffer holding the fields before substep j (vk_diffuse's rotation:

@@ -1,0 +1,326 @@
+"""Oracle (TEST INFRASTRUCTURE ONLY): the reference's multi-rate Experiment loop.
+
+A literal restatement, over nested dicts instead of Store objects, of
+  * Experiment.update ........ vivarium/core/experiment.py:1351-1450
+    (per-process fronts; a process runs when its front time <= time, with
+    timestep = min(front + local_timestep, interval) - front; the global
+    step is the smallest timestep that ran; updates whose front lands by
+    then are applied in front (first-appearance, depth-first) order; the
+    derivers run after every applied step; the no-process-ran jump keeps
+    the reference's use of the last loop path, :1414-1419)
+  * send_updates / run_derivers (derivers with timestep 0) ... :1319-1349
+  * Experiment.__init__'s initial deriver pass ................. :1247
+  * Store.apply_update for value updates: branches recurse, leaves apply
+    their schema updater or an inline {'_value', '_updater'} one, with a
+    port_mapping state for update_field_with_exchange ........... :586-739
+  * updaters accumulate / set / update_field_with_exchange .... vivarium/core/registry.py:117-183
+  * topology paths relative to the process's parent, '..' steps up
+    (normalize_path, experiment.py:1123-1130)
+Processes are invoked immediately (InvokeProcess, :1157-1167).  A '*' key in
+a ports schema applies to every child of that store (DiffusionField's
+agents schema, diffusion_field.py:292-302).
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from oracle.kinetics import N_A_LEGACY, bin_site, bin_volume_L, count_to_mM
+
+INFINITY = float('inf')
+
+
+def normalize_path(path):
+    progress = []
+    for step in path:
+        if step == '..' and progress:
+            progress = progress[:-1]
+        else:
+            progress.append(step)
+    return tuple(progress)
+
+
+def update_accumulate(current, new, states):
+    return current + new
+
+
+def update_set(current, new, states):
+    return new
+
+
+def make_update_field_with_exchange(avogadro=N_A_LEGACY):
+    def update_field_with_exchange(current, new, states):
+        location = states['global']['location']
+        dims = states['dimensions']
+        delta = np.zeros((dims['n_bins'][0], dims['n_bins'][1]), dtype=np.float64)
+        i, j = bin_site(location, dims['n_bins'], dims['bounds'])
+        delta[i, j] += count_to_mM(new, bin_volume_L(dims['n_bins'], dims['bounds'], dims['depth']), avogadro)
+        return current + delta
+    return update_field_with_exchange
+
+
+class OracleExperiment:
+    def __init__(self, processes, topology, initial_state, avogadro=N_A_LEGACY):
+        self.processes = processes
+        self.topology = topology
+        self.state = _copy_tree(initial_state)
+        self.updaters = {'accumulate': update_accumulate, 'set': update_set,
+                         'update_field_with_exchange': make_update_field_with_exchange(avogadro)}
+        self.schema = {}                      # store path (with '*' globs) -> updater name
+        self.local_time = 0.0
+        for path, proc in self._walk(processes, ()):
+            for port, port_schema in proc.ports_schema().items():
+                self._register(self.port_path(path, port), port_schema)
+        self.send_updates([])                 # the derivers run once at t = 0
+
+    # -- tree ------------------------------------------------------------------
+    def _walk(self, node, path):
+        out = []
+        for key, value in node.items():
+            if isinstance(value, dict):
+                out += self._walk(value, path + (key,))
+            else:
+                out.append((path + (key,), value))
+        return out
+
+    def _topology_of(self, path):
+        t = self.topology
+        for key in path:
+            t = t[key]
+        return t
+
+    def port_path(self, proc_path, port):
+        return normalize_path(proc_path[:-1] + tuple(self._topology_of(proc_path)[port]))
+
+    def get(self, path):
+        v = self.state
+        for key in path:
+            v = v[key]
+        return v
+
+    def _register(self, path, schema):
+        if not isinstance(schema, dict):
+            return
+        keys = [k for k in schema if not k.startswith('_')]
+        if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
+            if '_updater' in schema:           # a schema without one keeps the store's updater
+                self.schema.setdefault(path, schema['_updater'])
+            if '*' not in path:
+                node = self.state
+                for key in path[:-1]:
+                    node = node.setdefault(key, {})
+                if path[-1] not in node:
+                    node[path[-1]] = schema.get('_value', schema.get('_default'))
+            return
+        for k in keys:
+            self._register(path + (k,), schema[k])
+
+    def _updater_at(self, path):
+        if path in self.schema:
+            return self.schema[path]
+        for pat, name in self.schema.items():
+            if len(pat) == len(path) and all(p == '*' or p == q for p, q in zip(pat, path)):
+                return name
+        return 'accumulate'
+
+    # -- updates -------------------------------------------------------------
+    def process_states(self, path, proc):
+        return {port: self.get(self.port_path(path, port)) for port in proc.ports_schema()}
+
+    def apply_update(self, update, proc_path):
+        for port, value in update.items():
+            self._apply(self.port_path(proc_path, port), value, proc_path)
+
+    def _apply(self, path, update, proc_path):
+        parent = self.get(path[:-1])
+        if path[-1] not in parent:
+            return                                   # Store.apply_update skips unknown keys
+        current = parent[path[-1]]
+        inline = isinstance(update, dict) and '_updater' in update
+        if isinstance(current, dict) and not inline:
+            for key, value in update.items():
+                self._apply(path + (key,), value, proc_path)
+            return
+        states = None
+        if inline:
+            spec = update['_updater']
+            name, mapping = (spec, None) if isinstance(spec, str) else (spec['updater'], spec.get('port_mapping'))
+            value = update.get('_value')
+            if mapping is not None:
+                states = {up: self.get(self.port_path(proc_path, pp)) for up, pp in mapping.items()}
+        else:
+            name, value = self._updater_at(path), update
+        parent[path[-1]] = self.updaters[name](current, value, states)
+
+    def send_updates(self, updates, derivers=None):
+        for update, path in updates:
+            self.apply_update(update, path)
+        if derivers is None:
+            derivers = [(p, s) for p, s in self._walk(self.processes, ()) if s.is_deriver()]
+        for path, deriver in derivers:
+            update = deriver.next_update(0, self.process_states(path, deriver))
+            self.apply_update(update, path)
+
+    # -- Experiment.update ---------------------------------------------------
+    def update(self, interval):
+        time = 0
+        front = {}
+        while time < interval:
+            full_step = INFINITY
+            everything = self._walk(self.processes, ())
+            processes = [(p, s) for p, s in everything if not s.is_deriver()]
+            derivers = [(p, s) for p, s in everything if s.is_deriver()]
+            paths = {p for p, _ in processes}
+            front = {p: f for p, f in front.items() if p in paths}
+            for path, proc in processes:
+                if path not in front:
+                    front[path] = {'time': time, 'update': {}}
+                process_time = front[path]['time']
+                if process_time <= time:
+                    future = min(process_time + proc.local_timestep(), interval)
+                    timestep = future - process_time
+                    update = (proc.next_update(timestep, self.process_states(path, proc)), path)
+                    if timestep < full_step:
+                        full_step = timestep
+                    front[path]['time'] = future
+                    front[path]['update'] = update
+            if full_step == INFINITY:
+                next_event = interval
+                for _ in front.keys():
+                    if front[path]['time'] < next_event:       # the reference's stale `path`
+                        next_event = front[path]['time']
+                time = next_event
+            else:
+                future = time + full_step
+                updates = []
+                for path, advance in front.items():
+                    if advance['time'] <= future:
+                        updates.append(advance['update'])
+                        advance['update'] = {}
+                self.send_updates(updates, derivers)
+                time = future
+                self.local_time += full_step
+        return self
+
+
+def _copy_tree(t):
+    if isinstance(t, dict):
+        return {k: _copy_tree(v) for k, v in t.items()}
+    if isinstance(t, np.ndarray):
+        return t.copy()
+    if isinstance(t, list):
+        return list(t)
+    return t
+
+
+# ---------------------------------------------------------------------------
+# oracle processes
+# ---------------------------------------------------------------------------
+
+class OracleProcess:
+    """The parts of vivarium.core.process.Process (process.py:201-306) the loop uses."""
+    defaults = {}
+
+    def __init__(self, parameters=None):
+        self.parameters = dict(self.defaults)
+        self.parameters.update(parameters or {})
+
+    def local_timestep(self):
+        return self.parameters.get('time_step', 1.0)
+
+    def is_deriver(self):
+        return False
+
+
+class OracleConvenienceKinetics(OracleProcess):
+    """ConvenienceKinetics (convenience_kinetics.py:240-352) on oracle.kinetics.OracleAgent."""
+
+    def __init__(self, parameters):
+        super().__init__(parameters)
+        from oracle.kinetics import OracleAgent
+        self.agent = OracleAgent(parameters['reactions'], parameters['kinetic_parameters'])
+        self.initial_state = parameters.get('initial_state', {})
+
+    def ports_schema(self):
+        schema = {port: {} for port in ('internal', 'external', 'fluxes', 'fields', 'global', 'dimensions')}
+        for port, states in self.initial_state.items():
+            for k, v in states.items():
+                schema[port][k] = {'_default': v}
+        for rid in self.agent.model.reaction_ids:
+            schema['fluxes'][rid] = {'_default': 0.0, '_updater': 'set'}
+        return schema
+
+    def next_update(self, timestep, states):
+        st = {p: states[p] for p in ('internal', 'external')}
+        m2c = states['global']['mmol_to_counts']
+        fluxes, deltas, counts = self.agent.next_update(timestep, st, m2c)
+        update = {'fluxes': dict(fluxes), 'internal': deltas['internal']}
+        update['fields'] = {mol: {'_value': c, '_updater': {
+            'updater': 'update_field_with_exchange',
+            'port_mapping': {'global': 'global', 'dimensions': 'dimensions'}}} for mol, c in counts.items()}
+        return update
+
+
+class OracleDiffusionField(OracleProcess):
+    """DiffusionField.next_update (diffusion_field.py:280-407): field deltas and each
+    agent's external := the pre-step field at its bin."""
+    defaults = {'time_step': 1.0}
+
+    def __init__(self, parameters):
+        super().__init__(parameters)
+        self.molecules = list(parameters['molecules'])
+        self.n_bins = list(parameters['n_bins'])
+        self.bounds = list(parameters['bounds'])
+        self.diffusion = parameters['diffusion']
+        self.initial_state = parameters.get('initial_state', {})
+
+    def ports_schema(self):
+        return {
+            'agents': {'*': {'boundary': {
+                'location': {'_default': [0.5 * b for b in self.bounds], '_updater': 'set'},
+                'external': {m: {'_default': 0.0, '_updater': 'set'} for m in self.molecules}}}},
+            'fields': {m: {'_value': np.array(self.initial_state[m], dtype=np.float64) if m in self.initial_state
+                           else np.ones(self.n_bins), '_updater': 'accumulate'} for m in self.molecules},
+            'dimensions': {k: {'_value': self.parameters[k], '_updater': 'set'} for k in ('bounds', 'n_bins', 'depth')},
+        }
+
+    def next_update(self, timestep, states):
+        from oracle.lattice import diffusion_delta
+        fields = states['fields']
+        update = {'fields': {m: diffusion_delta(fields[m], timestep, self.diffusion, self.n_bins, self.bounds)
+                             for m in self.molecules}}
+        agents = states['agents']
+        if agents:
+            update['agents'] = {
+                aid: {'boundary': {'external': {
+                    m: fields[m][bin_site(spec['boundary']['location'], self.n_bins, self.bounds)]
+                    for m in self.molecules}}}
+                for aid, spec in agents.items()}
+        return update
+
+
+class OracleNonSpatialEnvironment(OracleProcess):
+    """NonSpatialEnvironment (nonspatial_environment.py:14-82): a deriver that sets
+    external[mol] := fields[mol][0][0]; 1 x 1 fields of bin volume = volume."""
+
+    def __init__(self, parameters):
+        super().__init__(parameters)
+        self.volume_L = parameters.get('volume_L', 1e-12)
+
+    def is_deriver(self):
+        return True
+
+    def ports_schema(self):
+        return {'external': {}, 'fields': {}, 'dimensions': {}, 'global': {}}
+
+    def next_update(self, timestep, states):
+        return {'external': {m: {'_updater': 'set', '_value': f[0][0]} for m, f in states['fields'].items()}}
+
+
+def nonspatial_dimensions(volume_L):
+    """The dimensions store NonSpatialEnvironment declares: 1 um x 1 um bins,
+    depth = volume / (1 um^2) in um (the expression oracle.kinetics.replay_single_agent
+    is pinned with against convenience_kinetics.csv)."""
+    return {'depth': volume_L * 1e15, 'n_bins': [1, 1], 'bounds': [1.0, 1.0]}

@@ -72,3 +72,20 @@ def lattice_step(fields, agents_loc, counts, n_bins, bounds, depth, timestep, di
             i, j = sites[a]
             f[i, j] = f[i, j] + count_to_mM(c, bvol, avogadro)
     return new, local
+
+
+def diffusion_delta(field, timestep, diffusion, n_bins, bounds, dt_max=0.01):
+    """DiffusionField.diffuse for one field (diffusion_field.py:385-407): the delta
+    field_new - field, zeros for a uniform field."""
+    if len(np.unique(field)) == 1:
+        return np.zeros_like(field)
+    dx = bounds[0] / n_bins[0]
+    dy = bounds[1] / n_bins[1]
+    coef = diffusion / (dx * dy)
+    fn = field.copy()
+    sub = min(timestep, dt_max)
+    t = 0.0
+    while t < timestep:
+        fn += coef * sub * laplacian_reflect(fn)
+        t += sub
+    return fn - field

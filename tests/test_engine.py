@@ -1,0 +1,136 @@
+"""The Experiment-shaped driver (lens_amd.engine) against the
+literal restatement of the reference's loop (oracle.experiment), on CPU.
+
+* the reference's own multi-rate scenario (experiment.py:1734-1801
+  test_timescales: a 3.0 s and a 0.3 s process on one store) plus a 0.7 s
+  process, run through both loops: identical states bit for bit;
+* BASELINE config 1 (convenience kinetics + NonSpatialEnvironment deriver)
+  through both loops reproduces the reference fixture convenience_kinetics.csv
+  -- which pins the restated scheduler, update order and updaters.
+"""
+
+import csv
+import os
+
+import numpy as np
+import pytest
+
+from lens_amd import configs
+from lens_amd.engine import Experiment
+from lens_amd.process import Process
+from oracle.experiment import (OracleConvenienceKinetics, OracleExperiment, OracleNonSpatialEnvironment,
+                               nonspatial_dimensions)
+from oracle.kinetics import mmol_to_counts
+
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+
+
+class Slow(Process):
+    name = 'slow'
+    defaults = {'timestep': 3.0}
+
+    def ports_schema(self):
+        return {'state': {'base': {'_default': 1.0}}}
+
+    def local_timestep(self):
+        return self.parameters['timestep']
+
+    def next_update(self, timestep, states):
+        return {'state': {'base': timestep * states['state']['base'] * 0.1}}
+
+
+class Fast(Process):
+    name = 'fast'
+    defaults = {'timestep': 0.3}
+
+    def ports_schema(self):
+        return {'state': {'base': {'_default': 1.0}, 'motion': {'_default': 0.0}}}
+
+    def local_timestep(self):
+        return self.parameters['timestep']
+
+    def next_update(self, timestep, states):
+        return {'state': {'motion': timestep * states['state']['base'] * 0.001}}
+
+
+class Odd(Process):
+    name = 'odd'
+    defaults = {'time_step': 0.7}
+
+    def ports_schema(self):
+        return {'state': {'motion': {'_default': 0.0}, 'tally': {'_default': 0.0, '_updater': 'set'}}}
+
+    def next_update(self, timestep, states):
+        return {'state': {'tally': states['state']['motion'] + timestep,
+                          'motion': -0.5 * timestep * states['state']['motion']}}
+
+
+def _timescales(loop, odd=True):
+    processes = {'slow': Slow(), 'fast': Fast()}
+    topology = {'slow': {'state': ('state',)}, 'fast': {'state': ('state',)}}
+    if odd:
+        processes['odd'] = Odd()
+        topology['odd'] = {'state': ('state',)}
+    init = {'state': {'base': 1.0, 'motion': 0.0}}
+    if loop is OracleExperiment:
+        return OracleExperiment(processes, topology, init)
+    return Experiment({'processes': processes, 'topology': topology, 'initial_state': init})
+
+
+@pytest.mark.parametrize('odd', [False, True])
+def test_multirate_loop_equals_reference_restatement(odd):
+    a, b = _timescales(Experiment, odd), _timescales(OracleExperiment, odd)
+    for interval in (10.0, 3.3, 0.05, 6.65):
+        a.update(interval)
+        b.update(interval)
+        assert a.state == b.state, interval
+        assert a.local_time == b.local_time
+    # the slow process really ran at its own rate: base grew 4 times in 10 s
+    c = _timescales(OracleExperiment, False).update(10.0)
+    base = 1.0
+    for dt in (3.0, 3.0, 3.0, 1.0):
+        base = base + dt * base * 0.1
+    assert c.state['state']['base'] == base
+
+
+def _c1(loop):
+    cfg = configs.glc_lct_config()
+    ports = ('internal', 'external', 'fluxes', 'fields', 'global', 'dimensions')
+    processes = {'kinetics': OracleConvenienceKinetics(cfg),
+                 'environment': OracleNonSpatialEnvironment({'volume_L': 1e-14})}
+    topology = {'kinetics': {p: (p,) for p in ports},
+                'environment': {p: (p,) for p in ('external', 'fields', 'dimensions', 'global')}}
+    init = {'internal': dict(cfg['initial_state']['internal']),
+            'external': dict(cfg['initial_state']['external']),
+            'fields': {m: np.ones((1, 1)) for m in cfg['initial_state']['external']},
+            'global': {'mmol_to_counts': mmol_to_counts(), 'location': [0.5, 0.5]},
+            'dimensions': nonspatial_dimensions(1e-14), 'fluxes': {}}
+    if loop is OracleExperiment:
+        return OracleExperiment(processes, topology, init)
+    return Experiment({'processes': processes, 'topology': topology, 'initial_state': init})
+
+
+@pytest.mark.parametrize('loop', [Experiment, OracleExperiment])
+def test_c1_through_the_loop_reproduces_reference_csv(loop):
+    rows = {int(float(r['time'])): r for r in csv.DictReader(open(os.path.join(GOLDEN,
+                                                                             'convenience_kinetics_subset.csv')))}
+    exp = _c1(loop)
+    for step in range(max(rows) + 1):
+        if step in rows:
+            for port in ('internal', 'external'):
+                for name, v in exp.state[port].items():
+                    ref = float(rows[step][port + '_' + name])
+                    tol = 1e-14 * abs(ref) if port == 'internal' else 1e-15
+                    assert abs(v - ref) <= tol, (step, port, name, v, ref)
+        exp.update(1.0)
+
+
+def test_c1_both_loops_bitwise():
+    a, b = _c1(Experiment), _c1(OracleExperiment)
+    for _ in range(50):
+        a.update(1.0)
+        b.update(1.0)
+    for port in ('internal', 'external', 'fluxes'):
+        assert a.state[port] == b.state[port]
+    for m in a.state['fields']:
+        assert np.array_equal(a.state['fields'][m], b.state['fields'][m])
