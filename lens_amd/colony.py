@@ -273,6 +273,88 @@ class Colony:
             self._env_to_external()
         self._finish_step(dt)
 
+    # -- multi-rate advance (Experiment.update, experiment.py:1351-1450) -------------
+    def run(self, interval: float, kinetics_dt: float = 1.0, diffusion_dt: float = 1.0):
+        """Advance a lattice colony by ``interval`` with the kinetics and the
+        diffusion field on their own clocks (each agent's kinetics process's
+        ``time_step``, the DiffusionField's ``time_step``), scheduled as the
+        reference's Experiment.update does: a process runs when its front time
+        <= time, with timestep = min(front + dt, interval) - front, and computes
+        its update from the state at that moment; the global step is the
+        smallest timestep that ran; updates whose front lands by then are
+        applied in store order -- the environment's (fields += delta, every
+        agent's external := the field at its bin when the diffusion ran)
+        before the agents' (internal += delta or := the DP45 end state,
+        fluxes, exchange into the field at apply time, in agent order).
+        ``run(dt, dt, dt)`` equals :meth:`step` (dt) bit for bit.
+        Cells (growth / division) step with :meth:`step`."""
+        if self.lattice is None:
+            raise ValueError('run() schedules a lattice colony; use step() otherwise')
+        if self.cells is not None:
+            raise ValueError('growth and division run with step(): their derivers fix one clock')
+        procs = [('diffusion', float(diffusion_dt)), ('kinetics', float(kinetics_dt))]   # store order
+        front = {name: 0.0 for name, _ in procs}      # every update() call starts its fronts at 0
+        pending = {}
+        time = 0.0
+        while time < interval:
+            full_step = float('inf')
+            for name, dt in procs:
+                f = front[name]
+                if f <= time:
+                    future = min(f + dt, interval)
+                    timestep = future - f
+                    pending[name] = self._compute(name, timestep)
+                    full_step = min(full_step, timestep)
+                    front[name] = future
+            future = time + full_step
+            for name, _ in procs:
+                if front[name] <= future and name in pending:
+                    self._apply(name, pending.pop(name))
+            time = future
+            self.time += full_step
+        self.step_index += 1
+        return self
+
+    def _compute(self, name, timestep):
+        """A process's update from the current state, not yet applied."""
+        lat, t = self.lattice, self.table
+        if name == 'diffusion':
+            delta = lat.diffuse_delta(timestep)
+            ext = torch.empty((t.n_species, self.ld), dtype=torch.float64, device=self.device)
+            lat.gather(self.bin_lin, self.n, self.map_gather_field, self.map_gather_row, ext)
+            return delta, ext
+        nd = t.n_dyn
+        flux = torch.empty_like(self.flux)
+        counts = torch.empty_like(self.counts)
+        if self.integrator == 'euler':
+            delta = torch.zeros((nd, self.ld), dtype=torch.float64, device=self.device)
+            self.engine.euler(timestep, self.params, self.conc, self.m2c, self.n, flux, counts, self.status,
+                              delta=delta)
+            return 'delta', delta, flux, counts
+        end = self.conc.clone()
+        self.engine.dopri5(timestep, self.params, end, self.m2c, self.n, self.h_state, self.rtol, self.atol,
+                           self.max_steps, flux, counts, self.status, self.nsteps)
+        return 'set', end[:nd], flux, counts
+
+    def _apply(self, name, update):
+        lat, t = self.lattice, self.table
+        n = self.n
+        if name == 'diffusion':
+            delta, ext = update
+            lat.fields.add_(delta)                      # the accumulate updater: field + delta
+            rows = self.map_gather_row.to(torch.int64)
+            self.conc[rows, :n] = ext[rows, :n]         # external: set
+            return
+        mode, value, flux, counts = update
+        nd = t.n_dyn
+        if mode == 'delta':
+            self.conc[:nd, :n] += value[:, :n]          # internal: accumulate
+        else:
+            self.conc[:nd, :n] = value[:, :n]
+        self.flux.copy_(flux)
+        self.counts.copy_(counts)
+        self._step_exchange()
+
     def _step_exchange(self):
         lat = self.lattice
         if self.map_exch_count.numel():

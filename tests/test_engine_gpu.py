@@ -149,3 +149,92 @@ def test_diffusion_field_process_update_dict_vs_oracle():
         assert got['agents'] == {k: {'boundary': {'external': {m: float(v) for m, v in
                                                                w['boundary']['external'].items()}}}
                                  for k, w in want['agents'].items()}
+
+
+# ---------------------------------------------------------------------------
+# the device-resident Colony on per-process clocks
+# ---------------------------------------------------------------------------
+
+def _lattice_colony(dev, integrator, n=60, nx=24, ny=20, seed=8):
+    from lens_amd import configs
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    from lens_amd.rate_law_compiler import compile_rate_laws
+    cfg = configs.glc_ac_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    rng = np.random.default_rng(seed)
+    loc = np.stack([rng.uniform(0, nx, n), rng.uniform(0, ny, n)])
+    loc[:, 4] = loc[:, 1]
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=seed)
+    glc = configs.gaussian_bump_field((nx, ny))
+    lat = Lattice(['glc__D_e', 'ac_e'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                  initial={'glc__D_e': glc, 'ac_e': np.zeros((nx, ny))})
+    col = Colony(cfg, n, device=dev, integrator=integrator, environment=lat, table=t)
+    col.set_agents(params=params, conc=conc, location=loc)
+    col.gather_external()
+    return cfg, t, col, lat, params, conc, loc, glc
+
+
+@pytest.mark.parametrize('integrator', ['euler', 'dopri5'])
+def test_colony_run_single_clock_equals_step(integrator):
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    _, _, a, la, *_ = _lattice_colony(dev, integrator)
+    _, _, b, lb, *_ = _lattice_colony(dev, integrator)
+    for _ in range(4):
+        a.step(1.0)
+        b.run(1.0, kinetics_dt=1.0, diffusion_dt=1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(a.conc, b.conc) and torch.equal(a.counts, b.counts) and torch.equal(a.flux, b.flux)
+    assert torch.equal(la.owned(), lb.owned())
+
+
+def test_colony_run_multirate_equals_reference_loop():
+    """Kinetics every 1 s, the diffusion field every 2.5 s (Euler): the device
+    colony's schedule equals the restated Experiment.update with oracle
+    processes, bit for bit, across several run() calls."""
+    from oracle.experiment import OracleConvenienceKinetics, OracleDiffusionField, OracleExperiment
+    from oracle.kinetics import params_dict
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    cfg, t, col, lat, params, conc, loc, glc = _lattice_colony(dev, 'euler')
+    n, (nx, ny) = col.n, lat.n_bins
+    m2c = col.m2c[:n].cpu().numpy()
+    ext0 = col.conc[:, :n].cpu().numpy()
+    env = {'molecules': ['glc__D_e', 'ac_e'], 'n_bins': [nx, ny], 'bounds': [float(nx), float(ny)],
+           'depth': 10.0, 'diffusion': 5.0, 'time_step': 2.5,
+           'initial_state': {'glc__D_e': glc, 'ac_e': np.zeros((nx, ny))}}
+    processes = {'diffusion': OracleDiffusionField(env), 'agents': {}}
+    topology = {'diffusion': {'agents': ('agents',), 'fields': ('fields',), 'dimensions': ('dimensions',)},
+                'agents': {}}
+    agents = {}
+    for a in range(n):
+        aid = 'a%03d' % a
+        kp = params_dict(t.param_names, cfg, params[:, a])
+        processes['agents'][aid] = {'kinetics': OracleConvenienceKinetics(dict(cfg, kinetic_parameters=kp,
+                                                                               time_step=1.0))}
+        topology['agents'][aid] = {'kinetics': {
+            'internal': ('internal',), 'external': ('boundary', 'external'), 'fluxes': ('fluxes',),
+            'fields': ('..', '..', 'fields'), 'dimensions': ('..', '..', 'dimensions'), 'global': ('boundary',)}}
+        agents[aid] = {
+            'internal': {k[1]: conc[s, a] for s, k in enumerate(t.species) if k[0] == 'internal'},
+            'fluxes': {},
+            'boundary': {'location': [loc[0, a], loc[1, a]], 'mmol_to_counts': m2c[a],
+                         'external': {k[1]: ext0[s, a] for s, k in enumerate(t.species) if k[0] == 'external'}}}
+    ref = OracleExperiment(processes, topology, {'agents': agents, 'dimensions': {
+        'bounds': env['bounds'], 'n_bins': env['n_bins'], 'depth': env['depth']}})
+    for interval in (3.0, 5.0, 1.5):
+        col.run(interval, kinetics_dt=1.0, diffusion_dt=2.5)
+        ref.update(interval)
+        torch.cuda.synchronize()
+        got = col.conc[:, :n].cpu().numpy()
+        for s, (port, name) in enumerate(t.species):
+            where = 'internal' if port == 'internal' else None
+            want = np.array([ref.state['agents']['a%03d' % a]['internal' if where else 'boundary']
+                             [name] if where else ref.state['agents']['a%03d' % a]['boundary']['external'][name]
+                             for a in range(n)])
+            assert np.array_equal(got[s], want), (interval, port, name)
+        for f, m in enumerate(lat.molecules):
+            assert np.array_equal(lat.owned(m).cpu().numpy(), ref.state['fields'][m]), (interval, m)
