@@ -42,7 +42,16 @@ WORKLOADS = {
     'c5': (1_000_000, 0, 0.0, 'BASELINE config 5: 50-species / 40-reaction network per agent (~85 integrated '
                               'components, agent-per-wavefront DP45) + Growth/DeriveGlobals/DivisionVolume '
                               'division events'),
+    'kremling': (1_000_000, 0, 0.0, 'BASELINE config 5 known-answer: the reference\'s stiff Kremling 2007 sugar '
+                                    'transport ODE (odeint path, 11 states + 4 flux integrals, 100-point output '
+                                    'grid per 1 s step), heterogeneous agents'),
 }
+
+# Kremling2007_transport.py:220-351 (oracle/kremling.rhs), counted as executed on the
+# G6P branch: uptake1 4, uptake2 13, hill 9, synthesis 11, rgly/rpdh 2, rpts 6,
+# f/rpyk 4, mu 3, derivatives 19 (a divide = 1 flop, XP**6 = 3 multiplies)
+KREMLING_RHS_FLOPS = 71
+KREMLING_NY = 15
 
 
 def stencil_kernel_name(variant, depth):
@@ -203,6 +212,113 @@ def cpu_baseline(args, col, host_state):
                           '; growth/division not included (negligible work)' if col.cells is not None else '')}
 
 
+def kremling_colony(n, dev, seed):
+    """Heterogeneous Kremling colony: GLC_G6P condition, internal x U(0.7, 1.3),
+    external x U(0.5, 1.5), volume U(0.5, 3) fL (tests/test_kremling.py's spread)."""
+    from lens_amd import kremling as lk
+    rng = np.random.default_rng(seed)
+    s0 = np.array([lk.GLC_G6P_INTERNAL[k] for k in lk.INTERNAL] + [lk.GLC_G6P_MEDIA[k] for k in lk.EXTERNAL])
+    states = np.repeat(s0[:, None], n, axis=1)
+    states[:8] *= rng.uniform(0.7, 1.3, (8, n))
+    states[8:11] *= rng.uniform(0.5, 1.5, (3, n))
+    col = lk.KremlingColony(n, device=dev)
+    col.set_state(states)
+    col.volume.copy_(torch.from_numpy(rng.uniform(0.5, 3.0, n)))
+    return col, states, col.volume.cpu().numpy()
+
+
+def cpu_baseline_odeint_worker(job):
+    """One agent-step through scipy's odeint (LSODA) on the restated right-hand side."""
+    kind, payload = job
+    if kind == 'kremling':
+        from oracle import kremling as ok
+        state, vol = payload
+        ok.step(np.asarray(state), volume_fL=vol)
+    else:
+        from oracle.kinetics import OracleODE, params_dict
+        cfg, param_names, pvec, conc, m2c = payload
+        ode = OracleODE(cfg['reactions'], params_dict(param_names, cfg, pvec))
+        ode.step(conc, 1.0, m2c, rtol=1e-8, atol=1e-12)
+    return 1
+
+
+def cpu_baseline_odeint(jobs, seconds, cores):
+    """SURVEY §8d CPU leg (ii): the reference's own algorithm -- scipy.integrate.odeint
+    (ODEPACK LSODA), one call per agent-step as Kremling2007_transport.py:384 makes
+    it -- on the restated right-hand side, over every host core (multiprocessing),
+    on a sample of the workload's agents, timed and scaled to agent-steps/s."""
+    from multiprocessing import get_context
+    with get_context('spawn').Pool(cores) as pool:       # fresh interpreters: nothing of the GPU process
+        pool.map(cpu_baseline_odeint_worker, jobs[:cores], chunksize=1)     # start-up off the clock
+        done, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            done += sum(pool.map(cpu_baseline_odeint_worker, jobs, chunksize=max(1, len(jobs) // (4 * cores))))
+        el = time.perf_counter() - t0
+    return {'value': done / el, 'unit': 'agent-steps/s', 'cores': cores, 'kind': 'port',
+            'sample': '%d agent-steps (%d sampled agents, repeated) through scipy odeint (LSODA) on the '
+                      'restated RHS, multiprocessing over %d cores, %.1f s' % (done, len(jobs), cores, el)}
+
+
+def run_kremling(args, rank, world, dev, dist):
+    n_total = getattr(args, 'agents', None) or WORKLOADS['kremling'][0]
+    n_local = n_total // world + (1 if rank < n_total % world else 0)
+    col, states, vols = kremling_colony(n_local, dev, configs.SEED + rank)
+    for _ in range(args.warmup):
+        col.step(1.0)
+    torch.cuda.synchronize()
+    col.check_status()
+    attempts = torch.zeros((), dtype=torch.int64, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(args.steps):
+        col.step(1.0)
+        attempts += col.nsteps.sum()
+    e1.record()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    col.check_status()
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    agents = torch.tensor([float(n_local * args.steps)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        if args.dist_backend == 'gloo':
+            el, agents = el.cpu(), agents.cpu()
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(agents, op=dist.ReduceOp.SUM)
+    if rank != 0:
+        return None
+    kms = e0.elapsed_time(e1) / args.steps
+    att = float(attempts.item()) / (n_local * args.steps)
+    flops_attempt = 6 * KREMLING_RHS_FLOPS + 64 * KREMLING_NY
+    tflops = att * flops_attempt * n_local / (kms * 1e-3) / 1e12
+    bytes_agent = 8 * (11 + 1 + 1) + 8 * (8 + 4 + 3 + 1) + 8
+    out = {
+        'metric': METRIC, 'value': float(agents.item()) / float(el.item()), 'unit': 'agent-steps/s',
+        'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': float(el.item()) / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'strong',
+        'vs_baseline': None, 'dtype': 'f64',
+        'data': 'synthetic (seeded heterogeneous Kremling colony around the reference GLC_G6P condition)',
+        'config': {'workload': WORKLOADS['kremling'][3], 'agents': n_total, 'dt_s': 1.0, 'output_grid': 100,
+                   'integrator': 'dopri5 landing on the odeint output grid', 'rtol': col.rtol, 'atol': col.atol,
+                   'parallelism': 'agents x%d' % world},
+        'roofline': {'bound': 'fp64-valu', 'kernel': 'k_kremling_step', 'achieved': tflops,
+                     'peak': FP64_PEAK_TFLOPS, 'unit': 'TFLOP/s', 'frac': tflops / FP64_PEAK_TFLOPS,
+                     'traffic': None, 'avg_launch_ms': kms, 'dp45_attempts_per_agent_step': att,
+                     'flops_per_attempt': flops_attempt,
+                     'hbm_gbps': n_local * bytes_agent / (kms * 1e-3) / 1e9},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        cores = int(os.environ.get('OMP_NUM_THREADS', '0') or 0) or len(os.sched_getaffinity(0))
+        jobs = [('kremling', (states[:, a].tolist() + [0.0] * 4, float(vols[a]))) for a in range(0, n_local, n_local // 256)]
+        out['cpu_baseline'] = cpu_baseline_odeint(jobs, args.cpu_seconds, cores)
+    return out
+
+
 def main():
     args = parse()
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -218,6 +334,14 @@ def main():
             dist.init_process_group('nccl', device_id=dev)       # RCCL over xGMI
         else:
             dist.init_process_group(args.dist_backend)
+    if args.workload == 'kremling':
+        out = run_kremling(args, rank, world, dev, dist)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     from lens_amd.lattice import stencil_depth, stencil_kernel
     stencil_depth(args.stencil_depth)
     if args.stencil_rows is None:
@@ -350,6 +474,16 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(args, col, host_state)
+            # leg (ii): the reference's own odeint on the restated RHS, sampled agents
+            params, conc, _ = host_state
+            t = col.table
+            cores = out['cpu_baseline']['cores']
+            stride = max(1, conc.shape[1] // 256)
+            jobs = [('convenience', (col.config, t.param_names, params[:, a].tolist(),
+                                     {k: float(conc[s_, a]) for s_, k in enumerate(t.species)},
+                                     float(col.m2c[a])))
+                    for a in range(0, conc.shape[1], stride)][:256]
+            out['cpu_baseline_odeint'] = cpu_baseline_odeint(jobs, min(8.0, args.cpu_seconds), cores)
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

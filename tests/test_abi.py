@@ -62,3 +62,20 @@ def _load_fresh(native, path):
         native.load(path)
     finally:
         native._lib = saved
+
+
+def test_bench_uses_the_oracle_only_in_its_cpu_baseline():
+    """bench.py may import oracle/ only inside its CPU-baseline functions (after the
+    timed GPU region), never to build or run the measured workload."""
+    import ast
+    tree = ast.parse(open(os.path.join(REPO, 'bench.py')).read())
+    for fn in ast.walk(tree):
+        if isinstance(fn, ast.FunctionDef):
+            for node in ast.walk(fn):
+                if isinstance(node, (ast.Import, ast.ImportFrom)):
+                    names = [a.name for a in node.names] + [getattr(node, 'module', None) or '']
+                    if any(n.split('.')[0] == 'oracle' for n in names):
+                        assert fn.name.startswith('cpu_baseline'), fn.name
+    top = [n for n in tree.body if isinstance(n, (ast.Import, ast.ImportFrom))]
+    assert not any('oracle' in (getattr(n, 'module', '') or '') or any('oracle' in a.name for a in n.names)
+                   for n in top)

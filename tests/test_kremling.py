@@ -100,3 +100,28 @@ def test_process_drop_in_update_dict(dev):
     assert [upd['fields'][m]['_value'] for m in ('GLC', 'G6P', 'LCTS')] == cnt.tolist()
     assert upd['fields']['GLC']['_updater']['updater'] == 'update_field_with_exchange'
     del GLC_G6P_MEDIA
+
+
+@pytest.mark.gpu
+def test_gpu_kremling_avogadro_is_a_parameter(dev):
+    """millimolar_to_counts reads scipy.constants.N_A at run time
+    (vivarium/library/flux_conversion.py:7,38): 6.022140857e23 under the scipy
+    the reference fixtures were made with, 6.02214076e23 from scipy 1.4 on.  The
+    kernel takes the constant as an argument; the exchange counts follow
+    whichever is passed (oracle with the same constant, +-1 count)."""
+    from lens_amd.kremling import KremlingColony
+    s0 = ok.initial_state()
+    n = 16
+    vol = np.linspace(0.5, 3.0, n)
+    got = {}
+    for na in (6.022140857e23, 6.02214076e23):
+        col = KremlingColony(n, device=dev, avogadro=na)
+        col.set_state(np.repeat(s0[:11, None], n, axis=1))
+        col.volume.copy_(torch.from_numpy(vol))
+        col.step(1.0)
+        col.check_status()
+        got[na] = col.counts.cpu().numpy()
+        for a in range(n):
+            cnt = ok.step(s0, volume_fL=vol[a], rtol=1e-13, atol=1e-16, avogadro=na)[2]
+            assert np.abs(got[na][:, a] - cnt).max() <= 1
+    assert (got[6.022140857e23] != got[6.02214076e23]).any()
