@@ -112,7 +112,7 @@ def test_gpu_kremling_avogadro_is_a_parameter(dev):
     from lens_amd.kremling import KremlingColony
     s0 = ok.initial_state()
     n = 16
-    vol = np.linspace(0.5, 3.0, n)
+    vol = np.linspace(1e7, 3e7, n)        # counts ~1e8: the two constants differ by ~1.3e-7 of them
     got = {}
     for na in (6.022140857e23, 6.02214076e23):
         col = KremlingColony(n, device=dev, avogadro=na)
