@@ -76,12 +76,13 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
 
 int g_stencil_rows = 64;   // output rows per wave tile (vk_stencil_kernels.h chunk_rows); 0 = auto
 // 0 = workgroup tile (LDS), 1 = wave tile (DPP), 2/3/4 = wave tile lag-1 prefetching 3/6/9 rows,
-// 5 = variant 3 capped at 4 waves/SIMD, 6/7 = variant 3 with streaming stores / loads+stores
+// 5 = variant 3 capped at 4 waves/SIMD, 6/7 = variant 3 with streaming stores / loads+stores,
+// 8 = four columns per lane (vk_stencil_wq.hip), 9 = 4 waves/SIMD lag-1 (vk_stencil_wlc.hip, even ny)
 static int g_stencil_kernel = 6;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant >= 0 && variant <= 7) g_stencil_kernel = variant;
+    if (variant >= 0 && variant <= 11) g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
 }
@@ -158,6 +159,18 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform, 0);
+        } else if (g_stencil_kernel == 11 && !(ny & 1) && k >= 3 && k <= 11) {
+            vk_launch_wlb(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                          bot_reflect, coeff_dt, uniform);
+        } else if (g_stencil_kernel == 10 && !(ny & 1) && k >= 3 && k <= 11) {
+            vk_launch_wls(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                          bot_reflect, coeff_dt, uniform);
+        } else if (g_stencil_kernel == 9 && !(ny & 1) && k >= 3 && k <= 11) {
+            vk_launch_wlc(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                          bot_reflect, coeff_dt, uniform);
+        } else if (g_stencil_kernel == 8 && k >= 3 && k <= 11) {
+            vk_launch_wq(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                         bot_reflect, coeff_dt, uniform);
         } else if (g_stencil_kernel >= 6 && (k == 7 || k == 9 || k == 11)) {
             (g_stencil_kernel == 6 ? vk_launch_wl6nt : vk_launch_wl6ntl)(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
                             bot_reflect, coeff_dt, uniform);
