@@ -58,12 +58,8 @@ def stencil_kernel_name(variant, depth):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
     if variant == 0:
         return 'k_diffuse_tb<%d>' % depth
-    if variant == 1:
-        return 'k_diffuse_wt<%d, false>' % depth
-    if variant == 5:
-        return 'k_diffuse_wl4<%d, 6, false>' % depth
-    if variant in (6, 7):
-        return '%s::k_diffuse_wl<%d, 6, false>' % ('vk_nt' if variant == 6 else 'vk_ntl', depth)
+    if variant == 6:
+        return 'vk_nt::k_diffuse_wl<%d, 6, false>' % depth
     return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 * (variant - 1))
 
 
@@ -81,8 +77,8 @@ def parse():
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
     p.add_argument('--stencil-kernel', type=int, default=6,
-                   help='0 workgroup/LDS, 1 wave/DPP lag-2, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows, '
-                        '5 = 3 capped at 4 waves/SIMD, 6/7 = 3 with streaming stores / loads+stores')
+                   help='0 workgroup/LDS, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows, '
+                        '6 = 3 with streaming stores (default)')
     p.add_argument('--stencil-depth', type=int, default=9)
     p.add_argument('--stencil-rows', type=int, default=None,
                    help='output rows per wave tile (default 64 on one GPU, 0 = auto on row bands)')

@@ -137,7 +137,7 @@ __global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__
 }
 
 // ---------------------------------------------------------------------------
-// Wave-tile variant: one wavefront = one independent tile of 128 columns (two
+// Wave tiles: one wavefront = one independent tile of 128 columns (two
 // adjacent columns per lane), so there is no LDS and no barrier at all.  The
 // left/right neighbours come from the lane itself (A<->B) and from the
 // adjacent lanes through DPP wave shifts (v_mov_b32_dpp wave_shr:1 /
@@ -188,144 +188,14 @@ struct WtLane {
 template <bool EDGE>
 __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t row_off, const WtLane &L) {
     if (!EDGE) {
-#ifdef VK_WL_NT_LOAD
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        const d2v w = __builtin_nontemporal_load(reinterpret_cast<const d2v *>(p + row_off + L.cA));
-        return make_double2(w.x, w.y);
-#else
         return *reinterpret_cast<const double2 *>(p + row_off + L.cA);
-#endif
     }
     const int a = min(max(L.cA, 0), L.ny - 1), b = min(max(L.cA + 1, 0), L.ny - 1);
     return make_double2(p[row_off + a], p[row_off + b]);
 }
 
-// STEADY: every stage is inside its useful row range (no fill/drain test),
-// so the K stages are straight-line code the scheduler can interleave.
-template <int K, bool EDGE, bool FINAL, bool STEADY, int U>
-__device__ __forceinline__ void wt_iter(double2 (&X0)[K], double2 (&X1)[K], double2 (&X2)[K], double2 (&pf)[3],
-                                        const double *__restrict__ s, double *d,
-                                        const double *g, const WtLane &L, int i, int c0, int c1,
-                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
-    double2(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
-    double2(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
-    double2(&NW)[K] = U == 0 ? X2 : (U == 1 ? X0 : X1);
-    const int64_t ny = L.ny;
-    NW[0] = pf[U];                                                                   // row i
-    pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny, L);  // prefetch row i+3
-    const int r_out = i - 2 * K + 1;
-    const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
-    double2 base = make_double2(0.0, 0.0);
-    if (FINAL && row_ok && (L.wA || L.wB)) base = wt_load<EDGE>(g, (int64_t)r_out * ny, L);
-#pragma unroll
-    for (int q = K - 1; q >= 0; --q) {
-        // stage q only matters for output rows [c0-(K-1-q), c1+(K-1-q)):
-        // skip the pipeline fill/drain iterations (wave-uniform branch)
-        if (!STEADY && (i < c0 - K + 3 * q + 2 || i > c1 + K - 1 + q)) continue;
-        const int r = i - 2 * q - 1;
-        const double2 cen = CN[q];
-        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
-        const double2 dn = (EDGE && r == bot_reflect) ? cen : NW[q];
-        double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
-        double rightA = cen.y, leftB = cen.x;
-        if (EDGE) {
-            leftA = L.lA ? cen.x : leftA;
-            rightA = L.rA ? cen.x : rightA;
-            leftB = L.lB ? cen.y : leftB;
-            rightB = L.rB ? cen.y : rightB;
-        }
-        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
-        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
-        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
-        if (q + 1 < K) {
-            UP[q + 1] = v;
-        } else if (row_ok) {
-            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
-            double *o = d + (int64_t)r_out * ny + L.cA;
-            if (!EDGE) {
-                if (L.wA) *reinterpret_cast<double2 *>(o) = v;
-            } else {
-                if (L.wA) o[0] = v.x;
-                if (L.wB) o[1] = v.y;
-            }
-        }
-    }
-}
-
-template <int K, bool EDGE, bool FINAL>
-__device__ __forceinline__ void diffuse_wt_body(const double *__restrict__ s, double *d,
-                                                const double *g, const WtLane &L, int c0, int c1,
-                                                int in_lo, int in_hi, int top_reflect, int bot_reflect,
-                                                double coef) {
-    double2 X0[K], X1[K], X2[K], pf[3];
-#pragma unroll
-    for (int q = 0; q < K; ++q) X0[q] = X1[q] = X2[q] = make_double2(0.0, 0.0);
-    const int i0 = c0 - K, i1 = c1 + 2 * K - 1;
-    const int64_t ny = L.ny;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
-    // iterations [s_lo, s_hi] have every stage active (fill ends, drain not begun)
-    const int s_lo = c0 + 2 * K - 1, s_hi = c1 + K - 1;
-#define WT_RUN(ST, U, I) wt_iter<K, EDGE, FINAL, ST, U>(X0, X1, X2, pf, s, d, g, L, I, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef)
-    int i = i0;
-    for (; i + 3 <= i1 && i < s_lo; i += 3) {   // fill
-        WT_RUN(false, 0, i); WT_RUN(false, 1, i + 1); WT_RUN(false, 2, i + 2);
-    }
-    for (; i + 2 <= s_hi; i += 3) {              // steady state: branch-free stages
-        WT_RUN(true, 0, i); WT_RUN(true, 1, i + 1); WT_RUN(true, 2, i + 2);
-    }
-    for (; i + 3 <= i1; i += 3) {                // drain
-        WT_RUN(false, 0, i); WT_RUN(false, 1, i + 1); WT_RUN(false, 2, i + 2);
-    }
-    if (i < i1) WT_RUN(false, 0, i);
-    if (i + 1 < i1) WT_RUN(false, 1, i + 1);
-#undef WT_RUN
-}
-
-template <int K, bool FINAL>
-__global__ __launch_bounds__(256) void k_diffuse_wt(const double *__restrict__ src, double *dst,
-                                                    const double *f0, int64_t field_stride, int ny,
-                                                    int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
-                                                    int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
-                                                    int n_fields, double coef, const double *__restrict__ uniform) {
-    constexpr int KH = K + (K & 1);           // even halo keeps 16-B alignment
-    constexpr int W = WT_COLS - 2 * KH;       // output columns per tile
-    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
-    const int lane = threadIdx.x & 63;
-    if (wave >= tiles_x * chunks_y * n_fields) return;
-    const int tx = wave % tiles_x;
-    const int ty = (wave / tiles_x) % chunks_y;
-    const int f = wave / (tiles_x * chunks_y);
-    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform plane: zero delta
-    const int c0 = out_lo + ty * rows_per_chunk;
-    const int c1 = min(c0 + rows_per_chunk, out_hi);
-    const int x0 = tx * W;                    // first output column
-    WtLane L;
-    L.ny = ny;
-    L.cA = x0 - KH + 2 * lane;
-    const int cB = L.cA + 1;
-    L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
-    L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
-    L.lA = L.cA == 0;
-    L.rA = L.cA == ny - 1;
-    L.lB = cB == 0;
-    L.rB = cB == ny - 1;
-    const double *s = src + (int64_t)f * field_stride;
-    double *d = dst + (int64_t)f * field_stride;
-    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
-    // reflecting boundaries or ragged columns inside the tile -> EDGE body
-    const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
-                      (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
-                      (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
-    if (edge)
-        diffuse_wt_body<K, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-    else
-        diffuse_wt_body<K, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
-}
-
 // ---------------------------------------------------------------------------
-// Wave-tile, lag-1 pipeline (variant 2).  Same tile / DPP scheme as
-// k_diffuse_wt, but stage q consumes stage q-1's output of the SAME iteration
+// Lag-1 pipeline (variants 2/3/4/6): stage q consumes stage q-1's output of the SAME iteration
 // (stage q computes row i-1-q at iteration i).  At the start of an iteration
 // each stage holds only two live rows (up, centre) instead of three, so the
 // register footprint drops from ~3K to ~2K row-pairs and more waves fit per
@@ -503,15 +373,6 @@ __global__ __launch_bounds__(256) void k_diffuse_wl(VK_WL_PARAMS) {
     diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
 }
 
-// Variant 5: the same tile with the register budget capped at 4 waves per SIMD
-// (128 VGPRs): the scheduler keeps fewer rows in flight per wave, and the
-// extra wave per SIMD overlaps one wave's row loads with another's stages.
-template <int K, int PD, bool FINAL>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_diffuse_wl4(VK_WL_PARAMS) {
-    diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
-}
-
-
 // Rows per wave tile: g_stencil_rows, or (auto) the largest <= 64 that still
 // yields ~4 waves per SIMD on the 1024 SIMDs -- small row bands (multi-GPU
 // strong scaling) trade pipeline fill for occupancy.
@@ -521,22 +382,3 @@ static int chunk_rows(int out_rows, int tiles_x, int nf) {
     int r = (int)(((int64_t)out_rows * tiles_x * nf) / want_waves);
     return std::max(16, std::min(64, r));
 }
-
-template <int K>
-static void launch_wt(hipStream_t st, const double *src, double *dst, const double *f0, int nf, int64_t fs,
-                      int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top, int bot, double coef,
-                      const double *mm) {
-    constexpr int KH = K + (K & 1);
-    constexpr int W = WT_COLS - 2 * KH;
-    const int tiles_x = (ny + W - 1) / W;
-    const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
-    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
-    const int waves = tiles_x * chunks_y * nf;
-    if (f0)
-        hipLaunchKernelGGL((k_diffuse_wt<K, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
-    else
-        hipLaunchKernelGGL((k_diffuse_wt<K, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm);
-}
-

@@ -16,11 +16,4 @@ void vk_launch_wl3(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 3 rows 
 void vk_launch_wl6(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 6 rows prefetched
 void vk_launch_wl9(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 9 rows prefetched
 void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS);        // as wl6 with streaming stores (k = 7, 9, 11)
-void vk_launch_wl6ntl(VK_STENCIL_LAUNCH_ARGS);       // as wl6nt with streaming loads too (k = 7, 9, 11)
-void vk_launch_wl4(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile capped at 4 waves/SIMD (k = 7, 9)
-void vk_launch_wq(VK_STENCIL_LAUNCH_ARGS);           // four columns per lane, 256-column tile (k = 3..11)
-void vk_launch_wlc(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile at 4 waves/SIMD (k = 3..11, even ny)
-void vk_launch_wls(VK_STENCIL_LAUNCH_ARGS);          // split-stage lag-1 wave tile (k = 3..11, even ny)
-void vk_launch_wlb(VK_STENCIL_LAUNCH_ARGS);          // split stages, bpermute neighbours (k = 3..11, even ny)
-void vk_launch_wt(VK_STENCIL_LAUNCH_ARGS);           // lag-2 wave tile
 void vk_launch_tb(VK_STENCIL_LAUNCH_ARGS);           // workgroup tile, LDS neighbour exchange

@@ -41,8 +41,9 @@ def stencil_depth(k: int = 0) -> int:
 
 
 def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
-    """Select the fused-pass kernel (0 = workgroup/LDS, 1 = wave/DPP lag-2, 2/3/4 = wave/DPP
-    lag-1 with 3/6/9 prefetched rows) and output rows per tile (0 = auto; -1 keeps)."""
+    """Select the fused-pass kernel (0 = workgroup/LDS, 2/3/4 = wave/DPP lag-1 with 3/6/9
+    prefetched rows, 6 = 3 with streaming stores, the default) and output rows per tile
+    (0 = auto; -1 keeps).  Other numbers are ignored (retired variants)."""
     native.load()
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
 

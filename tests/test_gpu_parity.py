@@ -291,13 +291,8 @@ def test_dopri5_wave_equals_lane_variant_small_network(dev):
     assert np.mean(out[0][1] == out[1][1]) > 0.99
 
 
-@pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (1, 3), (1, 7), (1, 11), (1, 15),
-                                           (2, 3), (2, 5), (2, 9), (2, 13), (2, 15), (3, 7), (3, 9),
-                                           (4, 5), (4, 11), (5, 7), (5, 9), (6, 7), (6, 9), (6, 11),
-                                           (7, 9), (6, 5), (8, 3), (8, 5), (8, 7), (8, 9), (8, 11),
-                                           (9, 3), (9, 5), (9, 7), (9, 9), (9, 11),
-                                           (10, 3), (10, 5), (10, 7), (10, 9), (10, 11),
-                                           (11, 3), (11, 5), (11, 7), (11, 9), (11, 11)])
+@pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (2, 3), (2, 5), (2, 9), (2, 13), (2, 15),
+                                           (3, 7), (3, 9), (4, 5), (4, 11), (6, 5), (6, 7), (6, 9), (6, 11)])
 def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
     """Every kernel variant and temporal-blocking depth reproduces
     scipy.ndimage.convolve bit for bit."""
@@ -321,14 +316,9 @@ def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
         stencil_kernel(prev_k, 64)
 
 
-@pytest.mark.parametrize('variant,depth,rows', [(0, 15, 64), (1, 15, 64), (1, 5, 256), (1, 9, 128),
-                                                (1, 13, 32), (1, 7, 512), (2, 9, 64), (2, 7, 128),
-                                                (2, 11, 32), (2, 15, 256), (3, 9, 64), (3, 13, 48),
-                                                (4, 9, 96), (4, 7, 40), (5, 9, 64), (6, 9, 64), (6, 11, 48),
-                                                (6, 7, 40), (7, 9, 96), (8, 7, 64), (8, 9, 40), (8, 11, 96),
-                                                (9, 7, 64), (9, 9, 40), (9, 5, 96), (9, 11, 24),
-                                                (10, 7, 64), (10, 9, 40), (10, 5, 96), (10, 11, 24),
-                                                (11, 7, 64), (11, 9, 40), (11, 5, 96), (11, 11, 24)])
+@pytest.mark.parametrize('variant,depth,rows', [(0, 15, 64), (2, 9, 64), (2, 7, 128), (2, 11, 32), (2, 15, 256),
+                                                (3, 9, 64), (3, 13, 48), (4, 9, 96), (4, 7, 40), (6, 9, 64),
+                                                (6, 11, 48), (6, 7, 40), (6, 9, 17)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
 def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
     """Multi-tile / multi-chunk geometry: interior tiles, ragged last tile and
