@@ -137,7 +137,12 @@ def path_timeseries_from_data(data):
 
 
 def process_path_timeseries_for_csv(path_ts):
-    """vivarium/library/timeseries.py:7-51: tuple keys joined with ',', non-numeric dropped."""
+    """vivarium/library/timeseries.py:7-51: tuple keys joined with ',', non-numeric dropped.
+
+    This and :func:`save_flat_timeseries` restate the reference's helpers nearly
+    line for line on purpose: they define the CSV wire format (key joining,
+    which columns are dropped, row padding), and the GPU colony must rebuild
+    ``reference_data/colony_metrics.csv`` byte for byte (tests/test_emitter.py)."""
     str_keys = {}
     for key, value in path_ts.items():
         if not isinstance(key, str):
