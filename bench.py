@@ -406,7 +406,7 @@ def main():
         n_total, nx, bound, desc = WORKLOADS[args.workload]
         integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
         variant = col.engine.default_variant()
-        kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec'}[variant]
+        kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec', 3: 'vk_dopri5_wspec'}[variant]
         integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / agent_steps,
                  'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),

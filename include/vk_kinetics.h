@@ -113,7 +113,11 @@ typedef struct vk_ode_opts {
                               wave-reduced error norm, wave-uniform step
                               control (n_dyn + n_reactions <= 512);
                           2 = agent-per-thread, network-specialised
-                              (vk_table_specialize)                          */
+                              (vk_table_specialize);
+                          3 = agent-per-wavefront, network-specialised:
+                              rate laws padded to one shape per round of 64
+                              lanes, per-lane operands in VGPRs
+                              (vk_table_specialize with a wavefront source) */
 } vk_ode_opts;
 
 int vk_abi_version(void);
@@ -123,9 +127,11 @@ int vk_table_create(const vk_table_desc *desc, vk_table **out);
 int vk_table_destroy(vk_table *table);
 
 /* Attach a network-specialised integrator to the table: `source` is the HIP
- * source lens_amd/codegen.py generates from the same table (straight-line
- * rate laws, every species/parameter/stage value in VGPRs); it is compiled
- * with hiprtc for gfx950.  vk_step_dopri5 uses it for opts->variant == 2. */
+ * source lens_amd/codegen.py generates from the same table, compiled with
+ * hiprtc for gfx950.  It defines `vk_dopri5_spec` (agent per lane: straight-
+ * line rate laws, every species/parameter/stage value in VGPRs; used for
+ * opts->variant == 2), `vk_dopri5_wspec` (agent per wavefront; variant 3),
+ * or both. */
 int vk_table_specialize(vk_table *table, const char *source);
 
 /* flux[r*ld + a] = sum over the reaction's rate laws (exact reference order). */
@@ -201,11 +207,10 @@ int vk_diffuse_delta(double *field, double *work0, double *work1, double *delta,
 int vk_set_stencil_depth(int32_t k);
 
 /* Fused-pass kernel variant: 0 = workgroup tile with an LDS neighbour
- * exchange; 1 = wave tile with DPP lane shifts, stage q lagging 2q rows;
- * 2 / 3 / 4 = wave tile, stage q lagging q rows (two live rows per stage),
- * 3 / 6 / 9 rows prefetched; 5 = variant 3 capped at 4 waves per SIMD;
- * 6 = variant 3 with streaming (non-temporal) stores (default); 7 = variant
- * 6 with streaming loads too.  rows = output rows per tile
+ * exchange; 2 / 3 / 4 = wave tile with DPP lane shifts, stage q lagging q
+ * rows (two live rows per stage), 3 / 6 / 9 rows prefetched; 6 = variant 3
+ * with streaming (non-temporal) stores (default).  Other values are ignored
+ * (retired variants 1, 5, 7-11).  rows = output rows per tile
  * (8..4096; 0 = auto from the band height; other values keep the current).
  * Returns the previous variant.  Tuning only: results are bit-identical for
  * every setting.                                                           */

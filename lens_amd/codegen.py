@@ -91,3 +91,135 @@ def dopri5_source(t: RateLawTable) -> str:
                .replace('@@RHS@@', rhs_body(t))
                .replace('@@COUNTS@@', counts_body(t))
                .replace('@@INVKM@@', invkm_body(t)))
+
+
+# ---------------------------------------------------------------------------
+# agent-per-wavefront specialisation (vk_dopri5_wave_spec.hip.in)
+# ---------------------------------------------------------------------------
+
+WAVE_TEMPLATE = os.environ.get('VK_DOPRI5_WAVE_TEMPLATE') or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), 'csrc', 'vk_dopri5_wave_spec.hip.in')
+WAVE_LANES = 64
+
+
+def wave_shape(t: RateLawTable) -> dict:
+    """The padded per-round rate-law shape and the per-lane table sizes."""
+    nl, nr, nd = t.n_rate_laws, t.n_reactions, t.n_dyn
+    ny = nd + nr
+
+    def sizes(ptr_lo, ptr_hi):
+        return [[int(t.set_ptr[s + 1] - t.set_ptr[s]) for s in range(ptr_lo[l], ptr_hi[l])] for l in range(nl)]
+
+    num = sizes(t.rl_num_ptr[:-1], t.rl_num_ptr[1:])
+    den = sizes(t.rl_den_ptr[:-1], t.rl_den_ptr[1:])
+    per_rx = [[l for l in range(nl) if int(t.rl_reaction[l]) == r] for r in range(nr)]
+    upd = [int(t.upd_ptr[i + 1] - t.upd_ptr[i]) for i in range(nd)]
+    return {
+        'LR': max(1, -(-nl // WAVE_LANES)),
+        'SN': max((len(x) for x in num), default=0),
+        'MN': max((m for x in num for m in x), default=0),
+        'SD': max((len(x) for x in den), default=0),
+        'MD': max((m for x in den for m in x), default=0),
+        'NSLOT': max(1, -(-ny // WAVE_LANES)),
+        'UM': max(upd, default=0),
+        'RX_IDENTITY': int(nl == nr and all(int(t.rl_reaction[l]) == l for l in range(nl))),
+        'RXR': max(1, -(-nr // WAVE_LANES)),
+        'RXM': max((len(x) for x in per_rx), default=0),
+        'num': num, 'den': den, 'per_rx': per_rx,
+    }
+
+
+def wave_registers(t: RateLawTable) -> int:
+    """Rough VGPR estimate of the specialised wave kernel (lane constants + DP45 state)."""
+    s = wave_shape(t)
+    lane = s['LR'] * (3 * s['SN'] * s['MN'] + 2 * s['SN'] + 1 + 3 * s['SD'] * s['MD']) + s['NSLOT'] * (1 + 3 * s['UM'])
+    return lane + 18 * s['NSLOT'] + 40
+
+
+def _table(name: str, ctype: str, rows) -> str:
+    """rows: list over outer dims of lists of 64-lane lists -> a C initializer."""
+    def fmt(v):
+        return repr(float(v)) if ctype == 'double' else str(int(v))
+
+    def rec(x):
+        if isinstance(x, (list, tuple)):
+            return '{' + ', '.join(rec(e) for e in x) + '}'
+        return fmt(x)
+
+    dims = []
+    x = rows
+    while isinstance(x, (list, tuple)):
+        dims.append(len(x))
+        x = x[0] if x else 0
+    dims = [max(d, 1) for d in dims]
+    if not rows or any(d == 0 for d in dims):
+        return '__device__ const %s %s%s = {};' % (ctype, name, ''.join('[%d]' % d for d in dims))
+    return '__device__ const %s %s%s = %s;' % (ctype, name, ''.join('[%d]' % d for d in dims), rec(rows))
+
+
+def wave_source(t: RateLawTable, wpe: int = 3) -> str:
+    """Complete HIP source of the specialised agent-per-wavefront kernel ``vk_dopri5_wspec``."""
+    sh = wave_shape(t)
+    W = WAVE_LANES
+    ns, nr, nl, nd = t.n_species, t.n_reactions, t.n_rate_laws, t.n_dyn
+    ny = nd + nr
+    LR, SN, MN, SD, MD = sh['LR'], sh['SN'], sh['MN'], sh['SD'], sh['MD']
+    PAD_SP = ns   # cl[NS] == 1.0
+    spn = [[[PAD_SP] * W for _ in range(max(SN * MN, 1))] for _ in range(LR)]
+    pin = [[[-1] * W for _ in range(max(SN * MN, 1))] for _ in range(LR)]
+    kc = [[[-1] * W for _ in range(max(SN, 1))] for _ in range(LR)]
+    enz = [[PAD_SP] * W for _ in range(LR)]
+    spd = [[[PAD_SP] * W for _ in range(max(SD * MD, 1))] for _ in range(LR)]
+    pid = [[[-1] * W for _ in range(max(SD * MD, 1))] for _ in range(LR)]
+    for l in range(nl):
+        r, lane = divmod(l, W)
+        enz[r][lane] = int(t.rl_enzyme[l])
+        for si, s in enumerate(range(t.rl_num_ptr[l], t.rl_num_ptr[l + 1])):
+            kc[r][si][lane] = int(t.rl_kcat[l])
+            for mi, m in enumerate(range(t.set_ptr[s], t.set_ptr[s + 1])):
+                spn[r][si * MN + mi][lane] = int(t.mem_species[m])
+                pin[r][si * MN + mi][lane] = int(t.mem_param[m])
+        for si, s in enumerate(range(t.rl_den_ptr[l], t.rl_den_ptr[l + 1])):
+            for mi, m in enumerate(range(t.set_ptr[s], t.set_ptr[s + 1])):
+                spd[r][si * MD + mi][lane] = int(t.mem_species[m])
+                pid[r][si * MD + mi][lane] = int(t.mem_param[m])
+    NSLOT, UM = sh['NSLOT'], sh['UM']
+    ui = [[nr] * W for _ in range(NSLOT)]
+    ur = [[[nr] * W for _ in range(max(UM, 1))] for _ in range(NSLOT)]
+    uc = [[[0.0] * W for _ in range(max(UM, 1))] for _ in range(NSLOT)]
+    for i in range(ny):
+        k, lane = divmod(i, W)
+        if i < nd:
+            for j, q in enumerate(range(t.upd_ptr[i], t.upd_ptr[i + 1])):
+                ur[k][j][lane] = int(t.upd_rxn[q])
+                uc[k][j][lane] = float(t.upd_coeff[q])
+        else:
+            ui[k][lane] = i - nd
+    RXR, RXM = sh['RXR'], sh['RXM']
+    rx = [[[nl] * W for _ in range(max(RXM, 1))] for _ in range(RXR)]
+    for r, ls in enumerate(sh['per_rx']):
+        rr, lane = divmod(r, W)
+        for j, l in enumerate(ls):
+            rx[rr][j][lane] = l
+    tables = '\n'.join([
+        _table('T_SPN', 'int', spn), _table('T_PIN', 'int', pin), _table('T_KC', 'int', kc),
+        _table('T_ENZ', 'int', enz), _table('T_SPD', 'int', spd), _table('T_PID', 'int', pid),
+        _table('T_UI', 'int', ui), _table('T_UR', 'int', ur), _table('T_UC', 'double', uc),
+        _table('T_RX', 'int', rx),
+    ])
+    defs = '\n'.join('#define %s %d' % (k, v) for k, v in [
+        ('NS', ns), ('ND', nd), ('NR', nr), ('NL', nl), ('NY', ny), ('LR', LR), ('SN', SN), ('MN', MN),
+        ('SD', SD), ('MD', MD), ('NSLOT', NSLOT), ('UM', UM), ('RX_IDENTITY', sh['RX_IDENTITY']),
+        ('RXR', RXR), ('RXM', RXM), ('TILE', ns + 1 + nr + 1 + nl + 1), ('WPE', wpe)])
+    umk = [max([int(t.upd_ptr[i + 1] - t.upd_ptr[i]) for i in range(k * W, min(nd, (k + 1) * W))] or [0])
+           for k in range(NSLOT)]
+    defs += '\n__device__ constexpr int UMK[NSLOT] = {%s};' % ', '.join(str(u) for u in umk)
+    counts = []
+    for e in range(t.n_ext):
+        terms = ['        c += trunc_count((%s * fl[%d]) * mc, cst);' % (_f(t.ex_coeff[j]), int(t.ex_rxn[j]))
+                 for j in range(t.ex_ptr[e], t.ex_ptr[e + 1])]
+        counts.append('    if (lane == %d) {\n        i64 c = 0;\n%s\n        counts[(i64)%d * ld + a] = c;\n    }'
+                      % (e % W, '\n'.join(terms), e))
+    with open(WAVE_TEMPLATE) as f:
+        src = f.read()
+    return src.replace('@@DEFS@@', defs).replace('@@TABLES@@', tables).replace('@@COUNTS@@', '\n'.join(counts))

@@ -29,7 +29,8 @@ struct vk_table {
     int32_t n_sets, n_members, n_upd, n_exch;
     int32_t n_ib, n_db;                    // element counts of the int / double blob parts
     hipModule_t spec_module = nullptr;     // vk_table_specialize (hiprtc)
-    hipFunction_t spec_dopri5 = nullptr;
+    hipFunction_t spec_dopri5 = nullptr;      // agent per lane (variant 2)
+    hipFunction_t spec_wave = nullptr;        // agent per wavefront (variant 3)
 };
 
 // Load through the constant address space: uniform index -> s_load (scalar cache).

@@ -207,15 +207,20 @@ extern "C" int vk_table_specialize(vk_table *t, const char *source) {
     hipModule_t mod;
     int rc = vk::hip_check(hipModuleLoadData(&mod, code.data()), "hipModuleLoadData(spec)");
     if (rc) return rc;
-    hipFunction_t fn;
-    rc = vk::hip_check(hipModuleGetFunction(&fn, mod, "vk_dopri5_spec"), "hipModuleGetFunction(spec)");
-    if (rc) {
+    // the source defines the agent-per-lane kernel, the agent-per-wavefront one, or both
+    hipFunction_t fn = nullptr, fw = nullptr;
+    if (hipModuleGetFunction(&fn, mod, "vk_dopri5_spec") != hipSuccess) fn = nullptr;
+    if (hipModuleGetFunction(&fw, mod, "vk_dopri5_wspec") != hipSuccess) fw = nullptr;
+    (void)hipGetLastError();
+    if (!fn && !fw) {
         (void)hipModuleUnload(mod);
-        return rc;
+        vk::set_error("vk_table_specialize: the source defines neither vk_dopri5_spec nor vk_dopri5_wspec");
+        return VK_ERR_ARG;
     }
     if (t->spec_module) (void)hipModuleUnload(t->spec_module);
     t->spec_module = mod;
     t->spec_dopri5 = fn;
+    t->spec_wave = fw;
     return VK_OK;
 }
 
@@ -976,6 +981,24 @@ extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double d
         return vk::hip_check(hipModuleLaunchKernel(t->spec_dopri5, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream,
                                                    args, nullptr),
                              "hipModuleLaunchKernel(vk_dopri5_spec)");
+    }
+    if (o->variant == 3) {  // network-specialised agent per wavefront (vk_table_specialize)
+        if (!t->spec_wave) {
+            vk::set_error("vk_step_dopri5: variant 3 needs vk_table_specialize with a wavefront source first");
+            return VK_ERR_ARG;
+        }
+        if (n > 0x1fffffff) {
+            vk::set_error("vk_step_dopri5: agent-per-wavefront grid limited to 2^29 agents");
+            return VK_ERR_LIMIT;
+        }
+        double rtol = o->rtol, atol = o->atol;
+        int max_steps = o->max_steps;
+        void *args[] = {&n, &ld, &dt, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c,
+                        &delta, &h_state, &flux, &counts, &status, &nsteps};
+        const unsigned blocks = (unsigned)((n + DW_WAVES - 1) / DW_WAVES);
+        return vk::hip_check(hipModuleLaunchKernel(t->spec_wave, blocks, 1, 1, DW * DW_WAVES, 1, 1, 0,
+                                                   (hipStream_t)stream, args, nullptr),
+                             "hipModuleLaunchKernel(vk_dopri5_wspec)");
     }
     const int ny = t->dev.n_dyn + t->dev.n_reactions;
     hipStream_t s = (hipStream_t)stream;

@@ -47,20 +47,27 @@ class KineticsEngine:
 
         Afterwards :meth:`dopri5` defaults to variant 2 (straight-line rate
         laws, everything in VGPRs) instead of the generic table walk."""
-        from lens_amd.codegen import dopri5_source
+        from lens_amd.codegen import dopri5_source, wave_registers, wave_source
         if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:
-            return self   # too large for one lane: the agent-per-wavefront kernel serves it
+            # too large for one lane: specialise the agent-per-wavefront kernel
+            # instead, while its padded per-lane operands fit the register file
+            if wave_registers(self.table) > self.WAVE_REGISTER_LIMIT:
+                return self
+            src = wave_source(self.table, self.WAVE_WAVES_PER_SIMD)
+        else:
+            src = dopri5_source(self.table)
         with torch.cuda.device(self.device):
-            native.check(native._lib.vk_table_specialize(self.dev.handle, dopri5_source(self.table).encode()),
-                         'vk_table_specialize')
+            native.check(native._lib.vk_table_specialize(self.dev.handle, src.encode()), 'vk_table_specialize')
         self.specialized = True
         return self
 
     LANE_LIMIT = 32   # integrated components an agent-per-lane kernel holds in VGPRs
+    WAVE_REGISTER_LIMIT = 270   # codegen.wave_registers estimate beyond which variant 1 stays (spills)
+    WAVE_WAVES_PER_SIMD = 3     # occupancy the specialised wavefront kernel is compiled for (C5: 2 -> 183 ms, 3 -> 131 ms)
 
     def default_variant(self) -> int:
         if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:
-            return 1
+            return 3 if self.specialized else 1
         return 2 if self.specialized else 0
 
     # -- allocation helpers -------------------------------------------------
@@ -120,7 +127,8 @@ class KineticsEngine:
 
         ``variant``: 0 = agent per lane, generic table walk; 1 = agent per
         wavefront (default when n_dyn + n_reactions > 32); 2 = agent per lane,
-        network-specialised (default once :meth:`specialize` ran).  Returns
+        network-specialised; 3 = agent per wavefront, network-specialised
+        (2 or 3 is the default once :meth:`specialize` ran).  Returns
         (flux = mean flux over dt, counts, status, nsteps)."""
         t = self.table
         if variant is None:

@@ -222,17 +222,28 @@ def _big_network(ns=50, nr=40, ne=10, n=160, seed=20261015):
     return cfg, t, params, conc
 
 
-@pytest.mark.parametrize('shape', [(50, 40, 10), (30, 20, 6), (120, 90, 12)])
-def test_dopri5_wave_vs_c_oracle(dev, shape):
+@pytest.mark.parametrize('variant', [1, 3])
+@pytest.mark.parametrize('shape', [(50, 40, 10), (30, 20, 6), (120, 90, 12), (90, 66, 33)])
+def test_dopri5_wave_vs_c_oracle(dev, shape, variant):
     """Agent-per-wavefront DP45 (C5-size networks) == the C oracle's DP45 to
     rounding: same RHS arithmetic, same step control; only the order of the
-    error norm's sum differs (a wave reduction)."""
+    error norm's sum differs (a wave reduction).  Variant 1 walks the table,
+    variant 3 is the network-specialised kernel (codegen.wave_source; the
+    90-species network needs two rounds of 64 rate-law lanes; the padded
+    operands of the 120-species one do not fit the register file, so
+    specialize() keeps the table walk for it)."""
+    from lens_amd import codegen
     cfg, t, params, conc = _big_network(*shape)
     n = conc.shape[1]
     assert t.n_dyn + t.n_reactions > 32
     m2c = np.full(n, mmol_to_counts())
     eng = _engine(t, dev)
-    assert eng.default_variant() == 1
+    if variant == 3:
+        eng.specialize()
+        if not eng.specialized:
+            assert codegen.wave_registers(t) > eng.WAVE_REGISTER_LIMIT
+            variant = 1
+    assert eng.default_variant() == variant
     c_dev = torch.from_numpy(conc.copy()).to(dev)
     h = torch.zeros(n, dtype=torch.float64, device=dev)
     flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev,
@@ -251,6 +262,67 @@ def test_dopri5_wave_vs_c_oracle(dev, shape):
     # exchange counts come from the flux integrals: equal up to a one-count
     # truncation flip where the integral sits on an integer boundary
     assert np.abs(counts.cpu().numpy() - k_ref).max() <= 1
+
+
+def _two_enzyme_network(n=96, seed=20261016):
+    """A C5-style network where every third reaction has a second catalyst:
+    reactions sum several rate laws (no one-to-one rate law/reaction map)."""
+    cfg = configs.synthetic_network(n_species=40, n_reactions=30, n_enzymes=8, seed=seed)
+    rng = np.random.default_rng(seed)
+    for i, (rid, spec) in enumerate(sorted(cfg['reactions'].items())):
+        if i % 3:
+            continue
+        first = spec['catalyzed by'][0]
+        second = ('internal', 'E%02d' % ((int(first[1][1:]) + 1) % 8))
+        spec['catalyzed by'] = [first, second]
+        p = dict(cfg['kinetic_parameters'][rid][first])
+        p['kcat_f'] = float(10 ** rng.uniform(-1, 3))
+        cfg['kinetic_parameters'][rid][second] = p
+    # an enzyme's partition holds the substrates of every reaction it catalyses
+    # (kinetic_rate_laws.py:84-95): each of its rate laws needs their Kms
+    for rid, spec in cfg['reactions'].items():
+        for enz in spec['catalyzed by']:
+            p = cfg['kinetic_parameters'][rid][enz]
+            for other in cfg['reactions'].values():
+                if enz in other['catalyzed by']:
+                    for m, c in other['stoichiometry'].items():
+                        if c < 0 and m not in p:
+                            p[m] = float(10 ** rng.uniform(-3, 1))
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    params, conc = configs.heterogeneous_colony(t, cfg, n, seed=seed + 1, sigma=0.2)
+    return cfg, t, params, conc
+
+
+@pytest.mark.parametrize('net', ['c5', 'two_enzyme', 'wide'])
+def test_dopri5_wave_spec_equals_generic_wave(dev, net):
+    """The specialised wavefront kernel (variant 3) against the table walk
+    (variant 1): the padded identities are exact and everything else is the
+    same arithmetic in the same order, so states, fluxes, counts, step counts
+    and carried step sizes agree bit for bit."""
+    from lens_amd import codegen
+    if net == 'c5':
+        cfg, t, params, conc = _big_network(n=300)
+    elif net == 'two_enzyme':
+        cfg, t, params, conc = _two_enzyme_network()
+        assert not codegen.wave_shape(t)['RX_IDENTITY'] and codegen.wave_shape(t)['RXM'] == 2
+    else:
+        cfg, t, params, conc = _big_network(90, 66, 33, n=64)
+        assert codegen.wave_shape(t)['LR'] == 2
+    n = conc.shape[1]
+    m2c = torch.full((n,), mmol_to_counts(), dtype=torch.float64, device=dev)
+    eng = _engine(t, dev)
+    out = []
+    for variant in (1, 3):
+        if variant == 3:
+            eng.specialize()
+        c_dev = torch.from_numpy(conc.copy()).to(dev)
+        h = torch.zeros(n, dtype=torch.float64, device=dev)
+        flux, counts, status, nsteps = eng.dopri5(1.0, torch.from_numpy(params).to(dev), c_dev, m2c, h_state=h,
+                                                  variant=variant)
+        out.append([x.cpu().numpy() for x in (c_dev, flux, counts, status, nsteps, h)])
+    for a, b, name in zip(out[0], out[1], ('conc', 'flux', 'counts', 'status', 'nsteps', 'h')):
+        assert np.array_equal(a, b), name
+    assert not out[1][3].any()
 
 
 def test_dopri5_wave_matches_odeint(dev):
