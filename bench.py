@@ -70,9 +70,9 @@ def parse():
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--workload', default='c4', choices=sorted(WORKLOADS))
     p.add_argument('--integrator', default='dopri5', choices=['dopri5', 'euler'])
-    p.add_argument('--halo', type=int, default=50,
-                   help='halo depth = substeps per halo exchange (multi-GPU; scripts/rank_emulate.py: '
-                        '50 beats 25 / 10 on 512-row bands)')
+    p.add_argument('--halo', type=int, default=None,
+                   help='halo depth = substeps per halo exchange (multi-GPU; default min(100, band rows): '
+                        'one exchange per step; scripts/halo_sweep.py, profiles/r02_halo_sweep/)')
     p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
@@ -112,7 +112,8 @@ def build_rank(args, rank, world, dev):
         n_local = n_total // world + (1 if rank < n_total % world else 0)
         glc = configs.gaussian_bump_field((nx, nx))
         lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (bound, bound), 10.0, 5.0, device=dev,
-                      row_band=band if world > 1 else None, halo=args.halo if world > 1 else 0,
+                      row_band=band if world > 1 else None,
+                      halo=(args.halo if args.halo is not None else min(100, band[1] - band[0])) if world > 1 else 0,
                       initial={'glc__D_e': glc, 'ac_e': np.zeros((nx, nx))})
         x = rng.uniform(band[0] * bound / nx, band[1] * bound / nx, n_local)
         y = rng.uniform(0.0, bound, n_local)
@@ -464,7 +465,7 @@ def main():
                        'substeps_per_step': n_substeps(1.0) if nx else 0,
                        'integrator': args.integrator, 'rtol': col.rtol, 'atol': col.atol,
                        'exchange': args.exchange, 'parallelism': 'row-bands x%d' % world,
-                       'halo': args.halo if world > 1 else 0},
+                       'halo': (col.lattice.halo if col.lattice is not None else 0) if world > 1 else 0},
             'roofline': roofline,
             'integrator': integ,
         }

@@ -373,12 +373,15 @@ __global__ __launch_bounds__(256) void k_diffuse_wl(VK_WL_PARAMS) {
     diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
 }
 
-// Rows per wave tile: g_stencil_rows, or (auto) the largest <= 64 that still
-// yields ~4 waves per SIMD on the 1024 SIMDs -- small row bands (multi-GPU
-// strong scaling) trade pipeline fill for occupancy.
+// Rows per wave tile: g_stencil_rows, or (auto) by the height of the rows the
+// pass writes -- small row bands (multi-GPU strong scaling) trade pipeline
+// fill for more waves.
 static int chunk_rows(int out_rows, int tiles_x, int nf) {
+    (void)tiles_x;
+    (void)nf;
     if (::g_stencil_rows > 0) return ::g_stencil_rows;
-    const int64_t want_waves = 4096;
-    int r = (int)(((int64_t)out_rows * tiles_x * nf) / want_waves);
-    return std::max(16, std::min(64, r));
+    // auto (row bands): the strong-scaling sweep of 4096^2 x 2 bands
+    // (scripts/halo_sweep.py, profiles/r02_halo_sweep/) is fastest with 64-row
+    // tiles on the whole plane, 32 on 1/2 and 1/4 bands, 16 on 1/8 bands
+    return out_rows >= 3000 ? 64 : (out_rows >= 1000 ? 32 : 16);
 }
