@@ -321,7 +321,7 @@ def test_c5_twenty_steps_vs_oracles(dev):
     step-start state), then gathered by the division order."""
     col, _, _ = bench.build_rank(_args('c5', 'dopri5', agents=4096), 0, 1, dev)
     cm = col.cells
-    assert col.engine.default_variant() == 1 and col.table.n_species >= 50
+    assert col.engine.default_variant() == 3 and col.table.n_species >= 50   # specialised wave kernel
     nd = col.table.n_dyn
     divisions = 0
     for step in range(20):
