@@ -146,8 +146,11 @@ class Lattice:
 
     def diffuse(self, timestep: float, halo_exchange: Optional[Callable] = None,
                 allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None,
-                before_final: Optional[Callable] = None):
+                before_final: Optional[Callable] = None, halo_ready: bool = False):
         """Advance every plane by ``timestep`` (diffusion_field.py:385-407).
+
+        ``halo_ready``: the caller already ran the first block's halo exchange
+        (see :meth:`exchange_first_halo`; the launch stream waits for it).
 
         ``events`` = (start, end) torch.cuda.Events recorded on the launch
         stream around the substep kernels only (bench roofline timing).
@@ -169,7 +172,7 @@ class Lattice:
         j = 0
         while j < n_sub:
             cnt = min(k, n_sub - j)
-            if banded:
+            if banded and not (halo_ready and j == 0):
                 halo_exchange(self.state_buffer(j), cnt)
             split = 0
             if before_final is not None and j + cnt == n_sub:
@@ -189,6 +192,21 @@ class Lattice:
         if events is not None:
             events[1].record()
         return n_sub
+
+    def exchange_first_halo(self, timestep: float, halo_exchange: Callable, stream):
+        """Run the halo exchange of :meth:`diffuse`'s first block on ``stream``
+        (a communication stream), so it overlaps what the launch stream does
+        meanwhile -- kinetics and the gather read only owned rows, the exchange
+        writes only halo rows.  Returns an event the launch stream must wait
+        on before ``diffuse(..., halo_ready=True)``."""
+        main = torch.cuda.current_stream(self.device)
+        stream.wait_stream(main)                       # the previous step's field
+        n_sub = n_substeps(timestep, self.diffusion_dt)
+        with torch.cuda.stream(stream):
+            halo_exchange(self.state_buffer(0), min(self.halo, n_sub))
+            done = torch.cuda.Event()
+            done.record()
+        return done
 
     def diffuse_delta(self, timestep: float, delta=None, allreduce=None):
         """DiffusionField.next_update's field delta (diffusion_field.py:385-407):
