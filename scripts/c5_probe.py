@@ -18,7 +18,7 @@ print('ny', t.n_dyn + t.n_reactions, 'rate laws', t.n_rate_laws, 'F_rhs', t.flop
 params, conc = configs.heterogeneous_colony(t, cfg, n, sigma=0.2)
 P = torch.from_numpy(params).to(dev)
 m2c = torch.full((n,), 7e5, dtype=torch.float64, device=dev)
-for label, variant, wpe in (('spec-3w', 3, 3), ('spec-4w', 3, 4), ('spec-5w', 3, 5), ('spec-3w', 3, 3)):
+for label, variant, wpe in (('generic', 1, None), ('spec-3w', 3, 3)):
     eng = KineticsEngine(t, dev)
     if wpe:
         eng.WAVE_WAVES_PER_SIMD = wpe
