@@ -83,6 +83,7 @@ class Experiment:
         self.avogadro = config.get('avogadro', N_A_LEGACY)
         self.state = _copy_tree(config.get('initial_state', {}))
         self.schema: Dict[Tuple, str] = {}
+        self._globs: List[Tuple] = []            # the schema paths holding a '*'
         self.updaters = {'accumulate': _accumulate, 'set': _set,
                          'update_field_with_exchange': self._update_field_with_exchange}
         self._exchange: Dict[Tuple, list] = {}      # device field path -> queued (location, dims, count)
@@ -124,6 +125,8 @@ class Experiment:
         if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
                 self.schema.setdefault(path, schema['_updater'])
+                if '*' in path and path not in self._globs:
+                    self._globs.append(path)
             if '*' not in path:
                 node = self.state
                 for key in path[:-1]:
@@ -137,9 +140,9 @@ class Experiment:
     def _updater_at(self, path):
         if path in self.schema:
             return self.schema[path]
-        for pat, name in self.schema.items():
+        for pat in self._globs:                  # '*' patterns, in registration order
             if len(pat) == len(path) and all(p == '*' or p == q for p, q in zip(pat, path)):
-                return name
+                return self.schema[pat]
         return 'accumulate'
 
     # -- updates ---------------------------------------------------------------

@@ -69,6 +69,7 @@ class OracleExperiment:
         self.updaters = {'accumulate': update_accumulate, 'set': update_set,
                          'update_field_with_exchange': make_update_field_with_exchange(avogadro)}
         self.schema = {}                      # store path (with '*' globs) -> updater name
+        self._globs = []                      # the schema paths holding a '*'
         self.local_time = 0.0
         for path, proc in self._walk(processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -107,6 +108,8 @@ class OracleExperiment:
         if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
                 self.schema.setdefault(path, schema['_updater'])
+                if '*' in path and path not in self._globs:
+                    self._globs.append(path)
             if '*' not in path:
                 node = self.state
                 for key in path[:-1]:
@@ -120,9 +123,9 @@ class OracleExperiment:
     def _updater_at(self, path):
         if path in self.schema:
             return self.schema[path]
-        for pat, name in self.schema.items():
+        for pat in self._globs:                  # '*' patterns, in registration order
             if len(pat) == len(path) and all(p == '*' or p == q for p, q in zip(pat, path)):
-                return name
+                return self.schema[pat]
         return 'accumulate'
 
     # -- updates -------------------------------------------------------------
