@@ -84,6 +84,7 @@ class Experiment:
         self.state = _copy_tree(config.get('initial_state', {}))
         self.schema: Dict[Tuple, str] = {}
         self._globs: List[Tuple] = []            # the schema paths holding a '*'
+        self._port_paths: Dict[Tuple, Tuple] = {}
         self.updaters = {'accumulate': _accumulate, 'set': _set,
                          'update_field_with_exchange': self._update_field_with_exchange}
         self._exchange: Dict[Tuple, list] = {}      # device field path -> queued (location, dims, count)
@@ -110,7 +111,11 @@ class Experiment:
         return t
 
     def port_path(self, proc_path, port):
-        return normalize_path(proc_path[:-1] + tuple(self._topology_of(proc_path)[port]))
+        key = (proc_path, port)
+        p = self._port_paths.get(key)
+        if p is None:
+            p = self._port_paths[key] = normalize_path(proc_path[:-1] + tuple(self._topology_of(proc_path)[port]))
+        return p
 
     def get(self, path):
         v = self.state
