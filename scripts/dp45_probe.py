@@ -18,7 +18,7 @@ import bench  # noqa: E402
 steps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 dev = torch.device('cuda', 0)
 args = types.SimpleNamespace(workload=os.environ.get('WORKLOAD', 'c4'), halo=0, integrator='dopri5',
-                             exchange='sorted', generic_kernel=False)
+                             exchange='sorted', generic_kernel=False, agents=None, overlap_kinetics=False)
 col, lat, _ = bench.build_rank(args, 0, 1, dev)
 ev = lambda: torch.cuda.Event(enable_timing=True)
 kin, eff, att = [], [], []
