@@ -284,7 +284,8 @@ class Colony:
         self._finish_step(dt)
 
     # -- multi-rate advance (Experiment.update, experiment.py:1351-1450) -------------
-    def run(self, interval: float, kinetics_dt: float = 1.0, diffusion_dt: float = 1.0):
+    def run(self, interval: float, kinetics_dt: float = 1.0, diffusion_dt: float = 1.0, halo_exchange=None,
+            allreduce=None):
         """Advance a lattice colony by ``interval`` with the kinetics and the
         diffusion field on their own clocks (each agent's kinetics process's
         ``time_step``, the DiffusionField's ``time_step``), scheduled as the
@@ -296,7 +297,8 @@ class Colony:
         agent's external := the field at its bin when the diffusion ran)
         before the agents' (internal += delta or := the DP45 end state,
         fluxes, exchange into the field at apply time, in agent order).
-        ``run(dt, dt, dt)`` equals :meth:`step` (dt) bit for bit.
+        ``run(dt, dt, dt)`` equals :meth:`step` (dt) bit for bit.  A row-banded
+        colony passes ``halo_exchange`` / ``allreduce`` as to :meth:`step`.
         Cells (growth / division) step with :meth:`step`."""
         if self.lattice is None:
             raise ValueError('run() schedules a lattice colony; use step() otherwise')
@@ -313,7 +315,7 @@ class Colony:
                 if f <= time:
                     future = min(f + dt, interval)
                     timestep = future - f
-                    pending[name] = self._compute(name, timestep)
+                    pending[name] = self._compute(name, timestep, halo_exchange, allreduce)
                     full_step = min(full_step, timestep)
                     front[name] = future
             future = time + full_step
@@ -325,11 +327,11 @@ class Colony:
         self.step_index += 1
         return self
 
-    def _compute(self, name, timestep):
+    def _compute(self, name, timestep, halo_exchange=None, allreduce=None):
         """A process's update from the current state, not yet applied."""
         lat, t = self.lattice, self.table
         if name == 'diffusion':
-            delta = lat.diffuse_delta(timestep)
+            delta = lat.diffuse_delta(timestep, allreduce=allreduce, halo_exchange=halo_exchange)
             ext = torch.empty((t.n_species, self.ld), dtype=torch.float64, device=self.device)
             lat.gather(self.bin_lin, self.n, self.map_gather_field, self.map_gather_row, ext)
             return delta, ext
@@ -351,7 +353,8 @@ class Colony:
         n = self.n
         if name == 'diffusion':
             delta, ext = update
-            lat.fields.add_(delta)                      # the accumulate updater: field + delta
+            own = slice(lat.row_lo, lat.row_hi)         # the accumulate updater: field + delta
+            lat.fields[:, own] += delta[:, own]
             rows = self.map_gather_row.to(torch.int64)
             self.conc[rows, :n] = ext[rows, :n]         # external: set
             return

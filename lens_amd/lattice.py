@@ -208,23 +208,38 @@ class Lattice:
             done.record()
         return done
 
-    def diffuse_delta(self, timestep: float, delta=None, allreduce=None):
+    def diffuse_delta(self, timestep: float, delta=None, allreduce=None, halo_exchange: Optional[Callable] = None):
         """DiffusionField.next_update's field delta (diffusion_field.py:385-407):
-        ``delta = new - field`` for every plane (zero for uniform planes), with
-        ``fields`` left as they were -- an accumulate updater applies it later
-        (vk_diffuse_delta).  Single-domain lattices only."""
-        if self.pad_top or self.pad_bot:
-            raise ValueError('diffuse_delta: a row band with halo rows is not supported')
+        ``delta = new - field`` for every plane (zero for uniform planes) on the
+        owned rows, with ``fields`` left as they were -- an accumulate updater
+        applies it later (vk_diffuse_delta).  A row band runs the halo blocks of
+        :meth:`diffuse` (``halo_exchange`` before each) and takes the delta in
+        its last block."""
+        banded = bool(self.pad_top or self.pad_bot)
+        if banded and halo_exchange is None:
+            raise ValueError('a row band with halo rows needs a halo_exchange callback')
         n_sub = n_substeps(timestep, self.diffusion_dt)
         coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
         mm = self.uniform_summary(allreduce)
         if delta is None:
             delta = torch.empty_like(self.fields)
-        native.check(native._lib.vk_diffuse_delta(
-            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1), native.ptr(delta),
-            len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, self.row_lo, self.row_hi,
-            int(self.edge_top), int(self.edge_bot), 0, n_sub, n_sub, coeff_dt, native.ptr(mm),
-            native.stream_handle()), 'vk_diffuse_delta')
+        lo_min = self.row_lo if self.edge_top else 0
+        hi_max = self.row_hi if self.edge_bot else self.rows_local
+        k = self.halo if banded else n_sub
+        j = 0
+        while j < n_sub:
+            cnt = min(k, n_sub - j)
+            if banded:
+                halo_exchange(self.state_buffer(j), cnt)
+            if j + cnt < n_sub:
+                self._run_block(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max)
+            else:
+                native.check(native._lib.vk_diffuse_delta(
+                    native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1), native.ptr(delta),
+                    len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, lo_min, hi_max,
+                    int(self.edge_top), int(self.edge_bot), j, cnt, n_sub, coeff_dt, native.ptr(mm),
+                    native.stream_handle()), 'vk_diffuse_delta')
+            j += cnt
         return delta
 
     def state_buffer(self, j: int):

@@ -276,3 +276,84 @@ def test_sharded_c5_with_rebalancing_equals_single_rank(world):
     assert sum(m for _, _, _, m in parts) > 0                  # rebalancing moved agents
     final = [len(st) for _, st, _, _ in parts]
     assert max(final) <= 1.02 * sum(final) / world + 1          # within the balancer's tolerance
+
+
+# ---------------------------------------------------------------------------
+# the multi-rate loop (Colony.run: kinetics and diffusion on their own clocks)
+# on row bands
+# ---------------------------------------------------------------------------
+
+RUNS = [(3.0, 1.0, 2.5), (5.0, 1.0, 2.5), (2.0, 0.5, 1.5), (4.0, 2.0, 1.0)]   # (interval, kinetics_dt, diffusion_dt)
+
+
+def _run_colony(dev, band, halo, integrator):
+    from lens_amd import configs
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    cfg, t, params, conc, loc, _, _ = _colony_inputs()
+    if band is not None:
+        rows = np.floor(loc[0]).astype(int)
+        mine = np.flatnonzero((rows >= band[0]) & (rows < band[1]))
+        params, conc, loc = params[:, mine], conc[:, mine], loc[:, mine]
+    lat = Lattice(['glc__D_e', 'ac_e'], (NX, NY), (float(NX), float(NY)), 10.0, 5.0, device=dev,
+                  row_band=band, halo=halo,
+                  initial={'glc__D_e': configs.gaussian_bump_field((NX, NY)), 'ac_e': np.zeros((NX, NY))})
+    col = Colony(cfg, conc.shape[1], device=dev, integrator=integrator, environment=lat, table=t)
+    col.set_agents(params=params, conc=conc, location=loc)
+    col.gather_external()
+    return col, lat
+
+
+def _run_worker(rank, world, port, halo, integrator, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from lens_amd.distributed import row_bands, make_halo_exchange, make_uniform_allreduce
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        band = row_bands(NX, world)[rank]
+        col, lat = _run_colony(dev, band, halo, integrator)
+        ex, ar = make_halo_exchange(lat, rank, world), make_uniform_allreduce()
+        hist = []
+        for interval, kdt, ddt in RUNS:
+            col.run(interval, kinetics_dt=kdt, diffusion_dt=ddt, halo_exchange=ex, allreduce=ar)
+            torch.cuda.synchronize()
+            hist.append((col.conc[:, :col.n].cpu().numpy().copy(), lat.owned().cpu().numpy().copy()))
+        q.put((rank, hist))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,halo,integrator', [(2, 20, 'euler'), (3, 7, 'dopri5')])
+def test_banded_multirate_run_equals_single_rank(world, halo, integrator):
+    """Colony.run on 2/3 row bands (banded vk_diffuse_delta with halo blocks,
+    kinetics and diffusion fronts as Experiment.update schedules them) equals
+    the single-domain run bit for bit, agent states and fields."""
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    col, lat = _run_colony(dev, None, 0, integrator)
+    ref = []
+    for interval, kdt, ddt in RUNS:
+        col.run(interval, kinetics_dt=kdt, diffusion_dt=ddt)
+        torch.cuda.synchronize()
+        ref.append((col.conc[:, :col.n].cpu().numpy().copy(), lat.owned().cpu().numpy().copy()))
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_run_worker, args=(r, world, port, halo, integrator, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=150) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for i in range(len(RUNS)):
+        conc = np.concatenate([hist[i][0] for _, hist in parts], axis=1)   # band-major = global order
+        fields = np.concatenate([hist[i][1] for _, hist in parts], axis=1)
+        assert np.array_equal(conc, ref[i][0]), i
+        assert np.array_equal(fields, ref[i][1]), i
