@@ -51,6 +51,7 @@ WORKLOADS = {
 # G6P branch: uptake1 4, uptake2 13, hill 9, synthesis 11, rgly/rpdh 2, rpts 6,
 # f/rpyk 4, mu 3, derivatives 19 (a divide = 1 flop, XP**6 = 3 multiplies)
 KREMLING_RHS_FLOPS = 71
+N_SIMDS = 256 * 4          # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 KREMLING_NY = 15
 
 
@@ -432,7 +433,7 @@ def main():
             launch_ms = stencil_pass_ms
             bytes_per_launch = 16.0 * cells          # algorithmic: read + write each cell once
             achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-            traffic = None
+            traffic = valu = None
             pmc = os.path.join(REPO, 'profiles', 'pmc_stencil.json')
             if os.path.exists(pmc) and world == 1:
                 with open(pmc) as f:
@@ -441,6 +442,14 @@ def main():
                 if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant')) == (
                         depth, args.stencil_rows, cells, args.stencil_kernel):
                     traffic = rec.get('hbm_bytes_per_launch')
+                    if rec.get('valu_insts_per_launch') and rec.get('clock_ghz'):
+                        # the pass against the VALU-issue bound: one wave64 VALU instruction
+                        # per 4 cycles per SIMD (1024 SIMDs) at the counter-measured clock,
+                        # for the counted instructions, over this run's launch time
+                        issue_s = rec['valu_insts_per_launch'] * 4.0 / (N_SIMDS * rec['clock_ghz'] * 1e9)
+                        valu = {'insts_per_launch': rec['valu_insts_per_launch'], 'clock_ghz': rec['clock_ghz'],
+                                'issue_bound_ms': issue_s * 1e3, 'frac': issue_s / (launch_ms * 1e-3),
+                                'busy_counter': rec.get('valu_busy_per_simd')}
             kname = stencil_kernel_name(args.stencil_kernel, depth)
             roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
@@ -449,7 +458,7 @@ def main():
                         'effective_stencil_gbps': bytes_per_launch * depth / (launch_ms * 1e-3) / 1e9,
                         'fp64_tflops': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12,
                         'fp64_frac': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                        'step_diffusion_ms': diff_ms}
+                        'valu_issue': valu, 'step_diffusion_ms': diff_ms}
         else:
             roofline = {'bound': 'fp64-valu', 'kernel': kname_i,
                         'achieved': integ.get('achieved_tflops'), 'peak': FP64_PEAK_TFLOPS,

@@ -1,7 +1,11 @@
 """Fold rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) for one stencil kernel into
 profiles/pmc_stencil.json, which bench.py reads for roofline.traffic.
 
-    python scripts/pmc_to_json.py KERNEL CELLS DEPTH ROWS VARIANT fetch.csv write.csv [out.json]
+    python scripts/pmc_to_json.py KERNEL CELLS DEPTH ROWS VARIANT fetch.csv write.csv [out.json] [--sq sq.csv]
+
+--sq: a pass with SQ_INSTS_VALU and GRBM_GUI_ACTIVE adds the VALU instructions
+per launch and the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / wall), from
+which bench.py reports the pass against the VALU-issue bound as well.
 
 FETCH_SIZE / WRITE_SIZE are KiB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of a wide
@@ -28,8 +32,14 @@ def mean_counter(path, kernel, counter):
     return sum(vals) / len(vals), len(vals)
 
 
-kernel, cells, depth, rows, variant, fcsv, wcsv = sys.argv[1:8]
-out = sys.argv[8] if len(sys.argv) > 8 else 'profiles/pmc_stencil.json'
+argv = list(sys.argv[1:])
+sq = None
+if '--sq' in argv:
+    i = argv.index('--sq')
+    sq = argv[i + 1]
+    del argv[i:i + 2]
+kernel, cells, depth, rows, variant, fcsv, wcsv = argv[:7]
+out = argv[7] if len(argv) > 7 else 'profiles/pmc_stencil.json'
 fetch_kib, nf = mean_counter(fcsv, kernel, 'FETCH_SIZE')
 write_kib, nw = mean_counter(wcsv, kernel, 'WRITE_SIZE')
 rec = {
@@ -41,5 +51,18 @@ rec = {
     'correction': 'FETCH_SIZE x2 (gfx950 wide-load undercount), WRITE_SIZE x1',
 }
 rec['hbm_bytes_per_launch'] = rec['read_bytes_per_launch'] + rec['write_bytes_per_launch']
+if sq:
+    per = {}
+    for r in csv.DictReader(open(sq)):
+        name = r['Kernel_Name']
+        if name.startswith(kernel) or name.startswith('void ' + kernel):
+            d = per.setdefault(r['Dispatch_Id'], {'ns': int(r['End_Timestamp']) - int(r['Start_Timestamp'])})
+            d[r['Counter_Name']] = d.get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
+    top = max(d['SQ_INSTS_VALU'] for d in per.values())
+    full = [d for d in per.values() if d['SQ_INSTS_VALU'] > 0.7 * top]
+    rec['valu_insts_per_launch'] = sum(d['SQ_INSTS_VALU'] for d in full) / len(full)
+    rec['clock_ghz'] = sum(d['GRBM_GUI_ACTIVE'] / 8 / d['ns'] for d in full) / len(full)
+    rec['valu_busy_per_simd'] = sum(d['SQ_ACTIVE_INST_VALU'] * 4 / 1024 / (d['GRBM_GUI_ACTIVE'] / 8)
+                                    for d in full) / len(full) if 'SQ_ACTIVE_INST_VALU' in full[0] else None
 json.dump(rec, open(out, 'w'), indent=1)
 print(json.dumps(rec))
