@@ -651,7 +651,7 @@ __global__ __launch_bounds__(DP_BS) void k_dopri5_thread(vk_dev_table t, int64_t
 // components.  The RMS error norm is a wavefront sum (DPP/shuffle butterfly),
 // so step acceptance, h and t are wave-uniform: no divergence at all.
 // Results agree with the lane kernels to rounding (only the order of the
-// norm's sum differs).
+// norm's sum differs: a pairwise tree here, a running sum there).
 
 constexpr int DW = 64;
 constexpr int DW_WAVES = 4;   // agents (waves) per workgroup
@@ -664,10 +664,50 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Wavefront sum, identical in every lane: a butterfly from the smallest
+// distance up.  Distances 1 and 2 are quad_perm DPP moves; once quads (then
+// 8-lane groups) hold equal values, row_half_mirror / row_mirror pair them
+// exactly as distances 4 / 8 would; distances 16 and 32 use the gfx950 row
+// swaps (v_permlane16/32_swap), after which each lane holds v[l] and
+// v[l ^ d] and adds them (FP addition commutes, so every lane gets the same
+// bits).  No LDS round trip, unlike __shfl_xor (ds_bpermute).
+__device__ __forceinline__ double dpp_pair(double v, int ctrl) {
+    int2 x = __builtin_bit_cast(int2, v);
+    int2 y;
+    switch (ctrl) {   // the DPP control must be a compile-time constant
+        case 0xB1:
+            y.x = __builtin_amdgcn_mov_dpp(x.x, 0xB1, 0xf, 0xf, false);
+            y.y = __builtin_amdgcn_mov_dpp(x.y, 0xB1, 0xf, 0xf, false);
+            break;
+        case 0x4E:
+            y.x = __builtin_amdgcn_mov_dpp(x.x, 0x4E, 0xf, 0xf, false);
+            y.y = __builtin_amdgcn_mov_dpp(x.y, 0x4E, 0xf, 0xf, false);
+            break;
+        case 0x141:
+            y.x = __builtin_amdgcn_mov_dpp(x.x, 0x141, 0xf, 0xf, false);
+            y.y = __builtin_amdgcn_mov_dpp(x.y, 0x141, 0xf, 0xf, false);
+            break;
+        default:
+            y.x = __builtin_amdgcn_mov_dpp(x.x, 0x140, 0xf, 0xf, false);
+            y.y = __builtin_amdgcn_mov_dpp(x.y, 0x140, 0xf, 0xf, false);
+            break;
+    }
+    return v + __builtin_bit_cast(double, y);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    v = dpp_pair(v, 0xB1);    // quad_perm [1,0,3,2]: lane ^ 1
+    v = dpp_pair(v, 0x4E);    // quad_perm [2,3,0,1]: lane ^ 2
+    v = dpp_pair(v, 0x141);   // row_half_mirror: the other quad of the 8-lane group
+    v = dpp_pair(v, 0x140);   // row_mirror: the other 8-lane group of the row
+    int2 x = __builtin_bit_cast(int2, v);
+    auto lo = __builtin_amdgcn_permlane16_swap(x.x, x.x, false, false);
+    auto hi = __builtin_amdgcn_permlane16_swap(x.y, x.y, false, false);
+    v = __builtin_bit_cast(double, make_int2(lo[0], hi[0])) + __builtin_bit_cast(double, make_int2(lo[1], hi[1]));
+    x = __builtin_bit_cast(int2, v);
+    lo = __builtin_amdgcn_permlane32_swap(x.x, x.x, false, false);
+    hi = __builtin_amdgcn_permlane32_swap(x.y, x.y, false, false);
+    return __builtin_bit_cast(double, make_int2(lo[0], hi[0])) + __builtin_bit_cast(double, make_int2(lo[1], hi[1]));
 }
 
 // rate law l from the agent's LDS tile (cl: species, pl: kcat or 1/Km);

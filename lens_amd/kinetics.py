@@ -63,7 +63,8 @@ class KineticsEngine:
 
     LANE_LIMIT = 32   # integrated components an agent-per-lane kernel holds in VGPRs
     WAVE_REGISTER_LIMIT = 270   # codegen.wave_registers estimate beyond which variant 1 stays (spills)
-    WAVE_WAVES_PER_SIMD = 3     # occupancy the specialised wavefront kernel is compiled for (C5: 2 -> 183 ms, 3 -> 131 ms)
+    WAVE_WAVES_PER_SIMD = 2     # occupancy the specialised wavefront kernel is compiled for: with its gathers
+                                # batched it needs 216 VGPRs (C5: 2 waves 120.5 ms; 3 waves spill, 224 ms)
 
     def default_variant(self) -> int:
         if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:
