@@ -82,11 +82,15 @@ def parse():
                         '6 = 3 with streaming stores (default)')
     p.add_argument('--stencil-depth', type=int, default=9)
     p.add_argument('--stencil-rows', type=int, default=None,
-                   help='output rows per wave tile (default 64 on one GPU, 0 = auto on row bands)')
+                   help='output rows per wave tile (default: 64 for C4 on one GPU, else 0 = auto by band height '
+                        'and wave count)')
     p.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
                    help='nccl (= RCCL) for real runs; gloo stages through host memory (rehearsal only)')
     p.add_argument('--overlap-kinetics', action='store_true',
                    help='run kinetics + gather on a side stream beside the diffusion passes')
+    p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
+                   help='replay the timed steps from a captured HIP graph (auto: launch-bound steps that take '
+                        'no host decision -- no division, no lattice or a single-GPU lattice up to 2048^2: C2, C3)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -342,8 +346,8 @@ def main():
         return
     from lens_amd.lattice import stencil_depth, stencil_kernel
     stencil_depth(args.stencil_depth)
-    if args.stencil_rows is None:
-        args.stencil_rows = 64 if world == 1 else 0
+    if args.stencil_rows is None:   # 64-row tiles on the whole 4096^2 plane, else the auto rule (chunk_rows)
+        args.stencil_rows = 64 if (world == 1 and args.workload == 'c4') else 0
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = balancer = None
@@ -377,24 +381,60 @@ def main():
         one_step(warm_timing[k])
     barrier()
     col.check_status()
-    col.attempts.zero_()
+    # HIP-graph replay: a step that is one small kinetics launch is host-bound
+    # when issued from Python; the graph holds `per_graph` steps
+    # (auto: launch-bound steps -- no lattice (C2) or a small one (C3); the C4 step is 2 ms of
+    # GPU work and keeps its per-step kernel timings)
+    small = lat is None or (world == 1 and (lat.row_hi - lat.row_lo) * lat.ny <= 2048 * 2048)
+    use_graph = (args.graph == 'on' or (args.graph == 'auto' and small and col.cells is None)) and balancer is None
+    graph_info = None
+    if use_graph:
+        per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
+        # the per-step attempt count (a reduction launch after each kinetics
+        # launch) is report bookkeeping, not workload: the graph leaves it out and
+        # the attempts are read from the last timed step's per-agent counts
+        col.count_attempts(False)
+        replay = col.capture(1.0, per_graph)
+        replay()             # uploads the graph; its steps are warmup, not timed
+        barrier()
+        col.check_status()
+        graph_info = {'steps_per_graph': per_graph, 'replays': args.steps // per_graph,
+                      'untimed_warmup_replay_steps': per_graph}
+    if col.attempts is not None:
+        col.attempts.zero_()
     agent_steps = 0          # agents integrated, summed over the timed steps (divisions grow n)
     n_start = col.n
     barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        agent_steps += col.n
-        one_step(timing[k])
+    if use_graph:
+        e_all = (ev(), ev())
+        t0 = time.perf_counter()
+        e_all[0].record()
+        for k in range(args.steps // per_graph):
+            agent_steps += col.n * per_graph
+            replay()
+        e_all[1].record()
+    else:
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            agent_steps += col.n
+            one_step(timing[k])
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()
     stencil_pass_ms = time_stencil_pass(lat, args.stencil_depth) if lat is not None else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
-    kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
+    if use_graph:           # no per-launch events inside a graph: the whole replayed step
+        kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps if lat is None else None
+    else:
+        kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
     diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
-               if lat is not None else 0.0)
-    attempts = float(col.attempts.item())
+               if lat is not None and not use_graph else None)
+    if use_graph:            # every timed step integrates the same agents (no division): last step x steps
+        attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
+        graph_info['attempts_from'] = 'per-agent attempt counts of the last timed step x steps'
+    else:
+        attempts = float(col.attempts.item())
     if dist is not None:
         if args.dist_backend == 'gloo':
             el, n_agents = el.cpu(), n_agents.cpu()
@@ -477,6 +517,7 @@ def main():
                        'halo': (col.lattice.halo if col.lattice is not None else 0) if world > 1 else 0},
             'roofline': roofline,
             'integrator': integ,
+            'hip_graph': graph_info,
         }
         if world == 1 and not args.no_cpu_baseline:
             out['cpu_baseline'] = cpu_baseline(args, col, host_state)

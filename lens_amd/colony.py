@@ -377,6 +377,42 @@ class Colony:
                 lat.exchange_atomic(self.bin_lin, self.n, self.counts, self.map_exch_count,
                                     self.map_exch_field)
 
+    def capture(self, dt: float = 1.0, steps: int = 1):
+        """Capture ``steps`` timesteps into one HIP graph (torch.cuda.CUDAGraph)
+        and return a function that replays them.
+
+        A small colony's step is a few short launches, and issuing them from
+        Python costs more than running them (C2: 40 µs per step issued, 4.5 µs
+        replayed). Replaying a captured graph leaves the host out of the loop.
+        Only steps that take no host decision can be captured: no division (the
+        host reads back the new agent count), no row band (its halo exchange
+        is a host-driven collective), no NonSpatialEnvironment and no
+        side-stream overlap. A single-GPU lattice step qualifies: the pass plan
+        depends only on Δt, and the uniform-plane skip is read by the kernels
+        from device memory. Capture records the launches without running them,
+        so the colony state is unchanged until the first replay."""
+        lat = self.lattice
+        if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
+                (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
+            raise ValueError('Colony.capture: division, row bands, NonSpatialEnvironment and side-stream overlap '
+                             'take host decisions per step and cannot be replayed from a graph')
+        if steps < 1:
+            raise ValueError('Colony.capture: steps >= 1')
+        graph = torch.cuda.CUDAGraph()
+        t0, s0 = self.time, self.step_index
+        with torch.cuda.graph(graph):
+            for _ in range(steps):
+                self.step(dt)
+        self.time, self.step_index = t0, s0      # capture ran nothing
+
+        def replay():
+            graph.replay()
+            self.time += dt * steps
+            self.step_index += steps
+
+        replay.graph = graph      # keep the graph (and its memory pool) alive with the replayer
+        return replay
+
     def _finish_step(self, dt):
         if self.cells is not None:
             self.grow_and_divide(dt)

@@ -74,7 +74,7 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
     }
 }
 
-int g_stencil_rows = 64;   // output rows per wave tile (vk_stencil_kernels.h chunk_rows); 0 = auto
+int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h chunk_rows); 0 = auto
 // 0 = workgroup tile (LDS neighbour exchange), 2/3/4 = wave tile lag-1 prefetching 3/6/9 rows,
 // 6 = variant 3 with streaming stores (the default).  Retired after A/B on the GPU:
 // 1 (lag-2 wave tile), 5 (4 waves/SIMD cap, spills), 7 (streaming loads), and the round-2

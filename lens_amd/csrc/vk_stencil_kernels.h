@@ -377,11 +377,14 @@ __global__ __launch_bounds__(256) void k_diffuse_wl(VK_WL_PARAMS) {
 // pass writes -- small row bands (multi-GPU strong scaling) trade pipeline
 // fill for more waves.
 static int chunk_rows(int out_rows, int tiles_x, int nf) {
-    (void)tiles_x;
-    (void)nf;
     if (::g_stencil_rows > 0) return ::g_stencil_rows;
-    // auto (row bands): the strong-scaling sweep of 4096^2 x 2 bands
-    // (scripts/halo_sweep.py, profiles/r02_halo_sweep/) is fastest with 64-row
-    // tiles on the whole plane, 32 on 1/2 and 1/4 bands, 16 on 1/8 bands
-    return out_rows >= 3000 ? 64 : (out_rows >= 1000 ? 32 : 16);
+    // auto: the strong-scaling sweep of 4096^2 x 2 bands (scripts/halo_sweep.py,
+    // profiles/r02_halo_sweep/) is fastest with 64-row tiles on the whole
+    // plane, 32 on 1/2 and 1/4 bands, 16 on 1/8 bands.  Narrower lattices have
+    // fewer tile columns: halve the rows until the pass has >= 1500 waves (a
+    // 1024^2 x 2 pass with 64-row tiles is 320 waves on 1024 SIMDs and takes
+    // 0.58 ms per 100 substeps; with 8-row tiles 0.35 ms, profiles/r02d_c3/)
+    int rows = out_rows >= 3000 ? 64 : (out_rows >= 1000 ? 32 : 16);
+    while (rows > 8 && (int64_t)tiles_x * ((out_rows + rows - 1) / rows) * nf < 1500) rows /= 2;
+    return rows;
 }

@@ -385,7 +385,7 @@ def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
                 assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))  # uniform skip
     finally:
         stencil_depth(prev)
-        stencil_kernel(prev_k, 64)
+        stencil_kernel(prev_k, 0)
 
 
 @pytest.mark.parametrize('variant,depth,rows', [(0, 15, 64), (2, 9, 64), (2, 7, 128), (2, 11, 32), (2, 15, 256),
@@ -405,7 +405,7 @@ def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
         lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
         lat.diffuse(1.0)
     finally:
-        stencil_kernel(prev, 64)
+        stencil_kernel(prev, 0)
         stencil_depth(prev_d)
     ref = np.ascontiguousarray(f0.copy())
     cpu.diffuse(ref, 5.0 * 0.01, 100)

@@ -1,0 +1,107 @@
+"""HIP-graph replay of a colony step (Colony.capture) against eager stepping (needs an MI355X)."""
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+
+from lens_amd import configs  # noqa: E402
+from lens_amd.rate_law_compiler import compile_rate_laws  # noqa: E402
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda', 0)
+
+
+def _colony(dev, n=5000):
+    from lens_amd.colony import Colony
+    cfg = configs.glc_lct_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    params, conc = configs.heterogeneous_colony(t, cfg, n)
+    col = Colony(cfg, n, device=dev, integrator='dopri5', table=t)
+    col.set_agents(params=params, conc=conc)
+    col.count_attempts(True)
+    return col
+
+
+def _state(col):
+    n = col.n
+    return {k: v[..., :n].cpu().numpy().copy() for k, v in
+            (('conc', col.conc), ('h', col.h_state), ('flux', col.flux), ('counts', col.counts),
+             ('nsteps', col.nsteps), ('attempts', col.attempts.reshape(1)))}
+
+
+@pytest.mark.parametrize('per_graph', [1, 4])
+def test_graph_replay_equals_eager_steps(dev, per_graph):
+    """C2-style colony (held externals, DP45): 8 steps replayed from a graph of
+    `per_graph` steps give the eager steps' state bit for bit, and the replayer
+    advances the colony clock."""
+    eager, graphed = _colony(dev), _colony(dev)
+    eager.step(1.0)                 # first use of the kernels in both colonies
+    graphed.step(1.0)
+    for _ in range(8):
+        eager.step(1.0)
+    before = _state(graphed)
+    replay = graphed.capture(1.0, per_graph)
+    torch.cuda.synchronize()
+    assert np.array_equal(_state(graphed)['conc'], before['conc'])   # capture runs nothing
+    for _ in range(8 // per_graph):
+        replay()
+    torch.cuda.synchronize()
+    eager.check_status()
+    graphed.check_status()
+    a, b = _state(eager), _state(graphed)
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert graphed.step_index == eager.step_index and graphed.time == eager.time
+
+
+def test_capture_refuses_host_decided_steps(dev):
+    """A lattice or division colony takes host decisions per step: capture refuses it."""
+    from lens_amd.colony import Colony
+    cfg = configs.glc_lct_config()
+    col = Colony(cfg, 4, device=dev, integrator='euler', environment='nonspatial')
+    with pytest.raises(ValueError):
+        col.capture(1.0, 1)
+
+
+def _lattice_colony(dev, n=3000, nx=200):
+    from lens_amd.colony import Colony
+    from lens_amd.lattice import Lattice
+    cfg = configs.glc_ac_config()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    rng = np.random.default_rng(5)
+    lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (float(nx), float(nx)), 10.0, 5.0, device=dev,
+                  initial={'glc__D_e': configs.gaussian_bump_field((nx, nx)), 'ac_e': np.zeros((nx, nx))})
+    params, conc = configs.heterogeneous_colony(t, cfg, n)
+    col = Colony(cfg, n, device=dev, integrator='dopri5', environment=lat, table=t, specialize=True)
+    col.set_agents(params=params, conc=conc, location=rng.uniform(0.0, float(nx), (2, n)))
+    col.gather_external()
+    return col
+
+
+def test_graph_replay_lattice_colony(dev):
+    """C3-style single-GPU lattice colony (kinetics, gather, 100 diffusion
+    substeps with the uniform-plane skip on the still-uniform acetate plane,
+    sorted exchange): 6 replayed steps equal 6 eager steps bit for bit."""
+    eager, graphed = _lattice_colony(dev), _lattice_colony(dev)
+    eager.step(1.0)
+    graphed.step(1.0)
+    for _ in range(6):
+        eager.step(1.0)
+    replay = graphed.capture(1.0, 3)
+    replay()
+    replay()
+    torch.cuda.synchronize()
+    eager.check_status()
+    graphed.check_status()
+    n = eager.n
+    assert np.array_equal(eager.conc[:, :n].cpu().numpy(), graphed.conc[:, :n].cpu().numpy())
+    assert np.array_equal(eager.counts[:, :n].cpu().numpy(), graphed.counts[:, :n].cpu().numpy())
+    for m in eager.lattice.molecules:
+        assert np.array_equal(eager.lattice.owned(m).cpu().numpy(), graphed.lattice.owned(m).cpu().numpy()), m
