@@ -16,49 +16,87 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stddef.h>
 #include <string.h>
+
+#include <mutex>
+#include <utility>
+#include <vector>
 
 #include "vk_internal.h"
 
 namespace {
 
-constexpr int KNY = 15;
+constexpr int KNY = 15;   // reference state: 11 species + 4 flux integrals
+constexpr int KS = 11;    // species: they feed the RHS
+// The four flux integrals (GLCpts, PPS, PYK, glc__D_e) never feed the RHS.
+// GLCpts and PPS integrate the same rate (uptake2) from 0, so they are equal
+// bit for bit and one of them is integrated (A0, counted twice in the error
+// norm and written to both rows).  Their stage inputs are never read, so
+// instead of seven stage vectors each keeps its 5th-order and error sums,
+// accumulated as the stages complete -- the same fma chain, in the same
+// order, as the species' b/e combinations.
+constexpr int KA = 3;     // integrated flux integrals: A0 = GLCpts (= PPS), A1 = PYK, A2 = glc__D_e
 
-struct Kp {  // device copy of vk_kremling_params
+struct Kp {  // device copy of vk_kremling_params plus host-derived constants
     double k1, k2, k3, K1, K2, K3, kd, m, n, x0, kg6p, Kg6p, kptsup, Kglc, Keiiap, klac, Km_lac, Kieiia;
     double kgly, kpyk, kpdh, kpts, km_pts, mw1, mw2, mw3, Y1_sim, Y2_sim, Y3_sim, K, kb, ksyn, KI;
+    double K6;        // K**6 (host pow)
+    double KglcKx0;   // Kglc * Keiiap * x0 (left to right, as the reference evaluates it)
+    int n_int, m_int; // the exponents n, m when they are small non-negative integers, else -1
 };
 
-// model(state, t) in the reference's operation order
-__device__ __forceinline__ void kremling_rhs(const Kp &p, const double (&s)[KNY], double (&d)[KNY]) {
+// division with the hardware reciprocal refined by two Newton steps (the
+// integrators' dp::fdiv; tolerance-parity, like every adaptive kernel here)
+__device__ __forceinline__ double kdiv(double a, double b) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(fma(-b, r, 1.0), r, r);
+    r = fma(fma(-b, r, 1.0), r, r);
+    return a * r;
+}
+
+// x**e for the model's exponents: repeated products for a small integer e
+// (the reference's defaults n = 2, m = 1), pow otherwise
+__device__ __forceinline__ double kpow(double x, double e, int ei) {
+    if (ei >= 0) {
+        double r = 1.0;
+        for (int i = 0; i < ei; ++i) r *= x;
+        return r;
+    }
+    return pow(x, e);
+}
+
+// model(state, t) in the reference's operation order (Kremling2007_transport.py:220-351)
+__device__ __forceinline__ void kremling_rhs(const Kp &p, const double (&s)[KS], double (&d)[KS], double (&da)[KA]) {
     const double biomass = s[0], UHPT = s[1], LACZ = s[2], PTSG = s[3], G6P = s[4], PEP = s[5], PYR = s[6],
                  XP = s[7], GLC_e = s[8], G6P_e = s[9], LCTS_e = s[10];
     const bool g6p = G6P > 0.01;
     double uptake1, transporter1;
     if (g6p) {
         transporter1 = UHPT;
-        uptake1 = p.kg6p * (transporter1 * G6P_e) / (p.Kg6p + G6P_e);
+        uptake1 = kdiv(p.kg6p * (transporter1 * G6P_e), p.Kg6p + G6P_e);
     } else {
         transporter1 = LACZ;
-        uptake1 = p.klac * (transporter1 * LCTS_e) /
-                  (p.Km_lac + LCTS_e * (1.0 + ((p.x0 - XP) / p.x0) / p.Kieiia));
+        uptake1 = kdiv(p.klac * (transporter1 * LCTS_e),
+                       p.Km_lac + LCTS_e * (1.0 + kdiv(kdiv(p.x0 - XP, p.x0), p.Kieiia)));
     }
-    const double uptake2 = p.kptsup * XP * (PTSG * GLC_e) /
-                           (p.Kglc * p.Keiiap * p.x0 + GLC_e * p.Keiiap * p.x0 + XP * p.Kglc + XP * GLC_e);
-    const double xp6 = pow(XP, 6.0);
-    const double hill = p.kb + p.ksyn * xp6 / (xp6 + pow(p.K, 6.0));
+    const double uptake2 = kdiv(p.kptsup * XP * (PTSG * GLC_e),
+                                p.KglcKx0 + GLC_e * p.Keiiap * p.x0 + XP * p.Kglc + XP * GLC_e);
+    const double xp2 = XP * XP;
+    const double xp6 = xp2 * xp2 * xp2;
+    const double hill = p.kb + kdiv(p.ksyn * xp6, xp6 + p.K6);
     double synthesis1, synthesis2;
     if (g6p) {
-        synthesis1 = p.k1 * hill * uptake1 / (p.K1 + uptake1);
-        synthesis2 = p.k2 * (p.KI / (transporter1 + p.KI)) * hill * uptake2 / (p.K2 + uptake2);
+        synthesis1 = kdiv(p.k1 * hill * uptake1, p.K1 + uptake1);
+        synthesis2 = kdiv(p.k2 * kdiv(p.KI, transporter1 + p.KI) * hill * uptake2, p.K2 + uptake2);
     } else {
-        synthesis1 = p.k3 * hill * uptake1 / (p.K3 + uptake1);
-        synthesis2 = p.k2 * hill * uptake2 / (p.K2 + uptake2);
+        synthesis1 = kdiv(p.k3 * hill * uptake1, p.K3 + uptake1);
+        synthesis2 = kdiv(p.k2 * hill * uptake2, p.K2 + uptake2);
     }
     const double rgly = p.kgly * G6P;
     const double rpdh = p.kpdh * PYR;
     const double rpts = p.kpts * PEP * (p.x0 - XP) - p.km_pts * PYR * XP;
-    const double f = pow(G6P, p.n) * pow(PEP, p.m);
+    const double f = kpow(G6P, p.n, p.n_int) * kpow(PEP, p.m, p.m_int);
     const double rpyk = p.kpyk * PEP * f;
     const double mu = (g6p ? p.Y1_sim : p.Y3_sim) * uptake1 + p.Y2_sim * uptake2;
     d[0] = mu * biomass;
@@ -72,10 +110,13 @@ __device__ __forceinline__ void kremling_rhs(const Kp &p, const double (&s)[KNY]
     d[8] = -p.mw2 * uptake2 * biomass;
     d[9] = g6p ? -p.mw1 * uptake1 * biomass : 0.0;
     d[10] = g6p ? 0.0 : -p.mw3 * uptake1 * biomass;
-    d[11] = uptake2;
-    d[12] = uptake2;
-    d[13] = rpyk;
-    d[14] = d[9];
+    da[0] = uptake2;   // GLCpts (and PPS)
+    da[1] = rpyk;      // PYK
+    da[2] = d[9];      // glc__D_e
+}
+
+__device__ __forceinline__ double step_factor(double en) {   // en ** -0.2
+    return exp2(-0.2 * log2(en));
 }
 
 namespace dpk {
@@ -91,9 +132,17 @@ constexpr double e1 = 71.0 / 57600.0, e3 = -71.0 / 16695.0, e4 = 71.0 / 1920.0, 
                  e6 = 22.0 / 525.0, e7 = -1.0 / 40.0;
 }  // namespace dpk
 
+// reference component i (0..14) of the error norm: species, then A0, A0 (PPS), A1, A2
+__device__ __forceinline__ int acc_of(int i) { return i == 11 || i == 12 ? 0 : i - 12; }
+
 }  // namespace
 
-__global__ __launch_bounds__(128) void k_kremling_dopri5(Kp p, int64_t n, int64_t ld, double grid_h, int n_grid,
+// 2 waves per SIMD (256 VGPRs).  The parameters come through a pointer to a
+// device copy, not by value: as a by-value argument they are pinned in SGPRs
+// and ~1,400 SGPR spills to VGPR lanes follow; through the pointer the
+// compiler re-loads them (s_load) where registers run short.
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_kremling_dopri5(
+                                                         const Kp *__restrict__ pp, int64_t n, int64_t ld, double grid_h, int n_grid,
                                                          double rtol, double atol, int max_steps,
                                                          double *__restrict__ state,
                                                          const double *__restrict__ volume_fl, double avogadro,
@@ -102,34 +151,39 @@ __global__ __launch_bounds__(128) void k_kremling_dopri5(Kp p, int64_t n, int64_
                                                          int32_t *__restrict__ nsteps_out) {
     const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= n) return;
-    double y[KNY], k1[KNY], k2[KNY], k3[KNY], k4[KNY], k5[KNY], k6[KNY], k7[KNY], yt[KNY];
+    const Kp &p = *pp;
+    double y[KS], k1[KS], k2[KS], k3[KS], k4[KS], k5[KS], k6[KS], k7[KS], yt[KS];
+    double ya[KA], k1a[KA], ka[KA], s5[KA], se[KA], yta[KA];
 #pragma unroll
-    for (int i = 0; i < 11; ++i) y[i] = state[(int64_t)i * ld + a];
+    for (int i = 0; i < KS; ++i) y[i] = state[(int64_t)i * ld + a];
 #pragma unroll
-    for (int i = 11; i < KNY; ++i) y[i] = 0.0;
+    for (int j = 0; j < KA; ++j) ya[j] = 0.0;
     const double c0_glc = y[8], c0_g6p = y[9], c0_lcts = y[10];
-    kremling_rhs(p, y, k1);
+    kremling_rhs(p, y, k1, k1a);
     int32_t st = 0;
     double h = h_state ? h_state[a] : 0.0;
     if (!(h > 0.0)) {   // scipy select_initial_step (order 4) over the first grid interval
         double d0 = 0.0, d1 = 0.0;
 #pragma unroll
         for (int i = 0; i < KNY; ++i) {
-            const double sc = fma(fabs(y[i]), rtol, atol);
-            d0 = fma(y[i] / sc, y[i] / sc, d0);
-            d1 = fma(k1[i] / sc, k1[i] / sc, d1);
+            const double yi = i < KS ? y[i] : ya[acc_of(i)], fi = i < KS ? k1[i] : k1a[acc_of(i)];
+            const double sc = fma(fabs(yi), rtol, atol);
+            d0 = fma(yi / sc, yi / sc, d0);
+            d1 = fma(fi / sc, fi / sc, d1);
         }
         d0 = sqrt(d0 / KNY);
         d1 = sqrt(d1 / KNY);
         double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 * grid_h : 0.01 * d0 / d1;
         h0 = fmin(h0, grid_h);
 #pragma unroll
-        for (int i = 0; i < KNY; ++i) yt[i] = fma(h0, k1[i], y[i]);
-        kremling_rhs(p, yt, k2);
+        for (int i = 0; i < KS; ++i) yt[i] = fma(h0, k1[i], y[i]);
+        kremling_rhs(p, yt, k2, ka);
         double d2 = 0.0;
 #pragma unroll
         for (int i = 0; i < KNY; ++i) {
-            const double q = (k2[i] - k1[i]) / fma(fabs(y[i]), rtol, atol);
+            const double yi = i < KS ? y[i] : ya[acc_of(i)];
+            const double df = i < KS ? k2[i] - k1[i] : ka[acc_of(i)] - k1a[acc_of(i)];
+            const double q = df / fma(fabs(yi), rtol, atol);
             d2 = fma(q, q, d2);
         }
         d2 = sqrt(d2 / KNY) / h0;
@@ -151,55 +205,84 @@ __global__ __launch_bounds__(128) void k_kremling_dopri5(Kp p, int64_t n, int64_
             if (tt + hs >= t_end) { hs = t_end - tt; last = true; }
             ++ns;
 #pragma unroll
-            for (int i = 0; i < KNY; ++i) yt[i] = fma(hs, dpk::a21 * k1[i], y[i]);
-            kremling_rhs(p, yt, k2);
+            for (int j = 0; j < KA; ++j) { s5[j] = dpk::b1 * k1a[j]; se[j] = dpk::e1 * k1a[j]; }
 #pragma unroll
-            for (int i = 0; i < KNY; ++i) yt[i] = fma(hs, fma(dpk::a32, k2[i], dpk::a31 * k1[i]), y[i]);
-            kremling_rhs(p, yt, k3);
+            for (int i = 0; i < KS; ++i) yt[i] = fma(hs, dpk::a21 * k1[i], y[i]);
+            kremling_rhs(p, yt, k2, ka);                      // b2 = e2 = 0
 #pragma unroll
-            for (int i = 0; i < KNY; ++i)
+            for (int i = 0; i < KS; ++i) yt[i] = fma(hs, fma(dpk::a32, k2[i], dpk::a31 * k1[i]), y[i]);
+            kremling_rhs(p, yt, k3, ka);
+#pragma unroll
+            for (int j = 0; j < KA; ++j) { s5[j] = fma(dpk::b3, ka[j], s5[j]); se[j] = fma(dpk::e3, ka[j], se[j]); }
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::a43, k3[i], fma(dpk::a42, k2[i], dpk::a41 * k1[i])), y[i]);
-            kremling_rhs(p, yt, k4);
+            kremling_rhs(p, yt, k4, ka);
 #pragma unroll
-            for (int i = 0; i < KNY; ++i)
+            for (int j = 0; j < KA; ++j) { s5[j] = fma(dpk::b4, ka[j], s5[j]); se[j] = fma(dpk::e4, ka[j], se[j]); }
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::a54, k4[i], fma(dpk::a53, k3[i], fma(dpk::a52, k2[i], dpk::a51 * k1[i]))), y[i]);
-            kremling_rhs(p, yt, k5);
+            kremling_rhs(p, yt, k5, ka);
 #pragma unroll
-            for (int i = 0; i < KNY; ++i)
+            for (int j = 0; j < KA; ++j) { s5[j] = fma(dpk::b5, ka[j], s5[j]); se[j] = fma(dpk::e5, ka[j], se[j]); }
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::a65, k5[i], fma(dpk::a64, k4[i], fma(dpk::a63, k3[i],
                             fma(dpk::a62, k2[i], dpk::a61 * k1[i])))), y[i]);
-            kremling_rhs(p, yt, k6);
+            kremling_rhs(p, yt, k6, ka);
 #pragma unroll
-            for (int i = 0; i < KNY; ++i)
+            for (int j = 0; j < KA; ++j) {
+                s5[j] = fma(dpk::b6, ka[j], s5[j]);
+                se[j] = fma(dpk::e6, ka[j], se[j]);
+                yta[j] = fma(hs, s5[j], ya[j]);
+            }
+#pragma unroll
+            for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::b6, k6[i], fma(dpk::b5, k5[i], fma(dpk::b4, k4[i],
                             fma(dpk::b3, k3[i], dpk::b1 * k1[i])))), y[i]);
-            kremling_rhs(p, yt, k7);
+            kremling_rhs(p, yt, k7, ka);                      // FSAL: k7 is the next step's k1
+#pragma unroll
+            for (int j = 0; j < KA; ++j) se[j] = fma(dpk::e7, ka[j], se[j]);
             double en = 0.0;
 #pragma unroll
             for (int i = 0; i < KNY; ++i) {
-                const double err = hs * fma(dpk::e7, k7[i], fma(dpk::e6, k6[i], fma(dpk::e5, k5[i],
-                                       fma(dpk::e4, k4[i], fma(dpk::e3, k3[i], dpk::e1 * k1[i])))));
-                const double q = err / fma(fmax(fabs(y[i]), fabs(yt[i])), rtol, atol);
+                double err, yo, yn;
+                if (i < KS) {
+                    err = hs * fma(dpk::e7, k7[i], fma(dpk::e6, k6[i], fma(dpk::e5, k5[i],
+                                   fma(dpk::e4, k4[i], fma(dpk::e3, k3[i], dpk::e1 * k1[i])))));
+                    yo = y[i];
+                    yn = yt[i];
+                } else {
+                    err = hs * se[acc_of(i)];
+                    yo = ya[acc_of(i)];
+                    yn = yta[acc_of(i)];
+                }
+                const double q = kdiv(err, fma(fmax(fabs(yo), fabs(yn)), rtol, atol));
                 en = fma(q, q, en);
             }
             en = sqrt(en / KNY);
             if (!isfinite(en)) { st |= VK_AGENT_NONFINITE; break; }
             if (en < 1.0) {
-                double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * pow(en, -0.2));
+                double factor = (en == 0.0) ? 10.0 : fmin(10.0, 0.9 * step_factor(en));
                 if (rejected) factor = fmin(1.0, factor);
                 tt = last ? t_end : tt + hs;
 #pragma unroll
-                for (int i = 0; i < KNY; ++i) { y[i] = yt[i]; k1[i] = k7[i]; }
+                for (int i = 0; i < KS; ++i) { y[i] = yt[i]; k1[i] = k7[i]; }
+#pragma unroll
+                for (int j = 0; j < KA; ++j) { ya[j] = yta[j]; k1a[j] = ka[j]; }
                 // landing on a grid point with a clipped step must not shrink h
                 h = last ? fmax(h, hs * factor) : hs * factor;
                 rejected = false;
             } else {
-                h = hs * fmax(0.2, 0.9 * pow(en, -0.2));
+                h = hs * fmax(0.2, 0.9 * step_factor(en));
                 rejected = true;
             }
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] += y[11 + j];
+        acc[0] += ya[0];
+        acc[1] += ya[0];
+        acc[2] += ya[1];
+        acc[3] += ya[2];
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -225,6 +308,30 @@ __global__ __launch_bounds__(128) void k_kremling_dopri5(Kp p, int64_t n, int64_
     if (nsteps_out) nsteps_out[a] = ns;
 }
 
+static int small_int(double e) {   // e as an exponent of repeated products, or -1
+    return (e >= 0.0 && e <= 8.0 && e == (double)(int)e) ? (int)e : -1;
+}
+
+// Device copies of the parameter sets in use, created at a set's first launch
+// (synchronous copy, so a launch captured into a graph later finds it) and
+// kept for the life of the process: colonies use a handful of sets.
+static std::mutex g_kp_mutex;
+static std::vector<std::pair<Kp, Kp *>> g_kp_sets;
+
+static int device_params(const Kp &p, const Kp **out) {
+    std::lock_guard<std::mutex> lock(g_kp_mutex);
+    for (auto &e : g_kp_sets)
+        if (memcmp(&e.first, &p, sizeof(Kp)) == 0) { *out = e.second; return VK_OK; }
+    Kp *d = nullptr;
+    int rc = vk::hip_check(hipMalloc(&d, sizeof(Kp)), "hipMalloc(kremling params)");
+    if (rc) return rc;
+    rc = vk::hip_check(hipMemcpy(d, &p, sizeof(Kp), hipMemcpyHostToDevice), "hipMemcpy(kremling params)");
+    if (rc) { (void)hipFree(d); return rc; }
+    g_kp_sets.emplace_back(p, d);
+    *out = d;
+    return VK_OK;
+}
+
 extern "C" int vk_kremling_step(const vk_kremling_params *kp, int64_t n, int64_t ld, double timestep_h,
                                 double grid_h, int32_t n_grid, double rtol, double atol, int32_t max_steps,
                                 double *state, const double *volume_fl, double avogadro, double *h_state,
@@ -238,9 +345,17 @@ extern "C" int vk_kremling_step(const vk_kremling_params *kp, int64_t n, int64_t
     (void)timestep_h;
     if (n == 0) return VK_OK;
     Kp p;
-    static_assert(sizeof(Kp) == sizeof(vk_kremling_params), "parameter layout");
-    memcpy(&p, kp, sizeof(Kp));
-    hipLaunchKernelGGL(k_kremling_dopri5, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, (hipStream_t)stream, p,
+    memset(&p, 0, sizeof(Kp));   // padding too: parameter sets are compared bytewise
+    static_assert(offsetof(Kp, K6) == sizeof(vk_kremling_params), "parameter layout");
+    memcpy(&p, kp, sizeof(vk_kremling_params));
+    p.K6 = pow(kp->K, 6.0);
+    p.KglcKx0 = kp->Kglc * kp->Keiiap * kp->x0;
+    p.n_int = small_int(kp->n);
+    p.m_int = small_int(kp->m);
+    const Kp *dp = nullptr;
+    int rc = device_params(p, &dp);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_kremling_dopri5, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, (hipStream_t)stream, dp,
                        n, ld, grid_h, n_grid, rtol, atol, max_steps, state, volume_fl, avogadro, h_state, flux,
                        counts, status, nsteps);
     return vk::launch_check("k_kremling_dopri5");
