@@ -165,6 +165,26 @@ def time_stencil_pass(lat, depth, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+def time_copy_floor(lat, reps=20):
+    """Average duration of a plain device copy of the planes a pass streams
+    (fields -> work0: one 8-B read + one 8-B write per cell, the algorithmic
+    bytes of one fused pass), HIP events on the launch stream.  The measured
+    floor any pass has on this box (scripts/micro/stencil_mem.hip: a
+    hand-written 16-B-per-lane streaming copy measures the same 5.5 TB/s)."""
+    src = lat.fields.reshape(-1)
+    dst = lat.work0.reshape(-1)
+    for _ in range(3):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps, 16.0 * src.numel()
+
+
 def cpu_baseline(args, col, host_state):
     """The oracle's C restatement (OpenMP) on this host, on a bounded sample of
     the same workload: whole steps, repeated until ~cpu_seconds have passed."""
@@ -422,6 +442,7 @@ def main():
     elapsed = time.perf_counter() - t0
     col.check_status()
     stencil_pass_ms = time_stencil_pass(lat, args.stencil_depth) if lat is not None else None
+    copy_floor = time_copy_floor(lat) if lat is not None and world == 1 else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
     if use_graph:           # no per-launch events inside a graph: the whole replayed step
@@ -499,6 +520,13 @@ def main():
                         'fp64_tflops': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12,
                         'fp64_frac': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
                         'valu_issue': valu, 'step_diffusion_ms': diff_ms}
+            if copy_floor is not None:
+                # the pass against the HBM rate this box delivers to a plain streaming copy of
+                # the same planes (8 TB/s is the spec; a copy reaches ~5.5)
+                cms, cbytes = copy_floor
+                floor_ms = cms * bytes_per_launch / cbytes
+                roofline['copy_floor'] = {'copy_ms': cms, 'copy_gbps': cbytes / (cms * 1e-3) / 1e9,
+                                          'floor_ms_per_launch': floor_ms, 'frac': floor_ms / launch_ms}
         else:
             roofline = {'bound': 'fp64-valu', 'kernel': kname_i,
                         'achieved': integ.get('achieved_tflops'), 'peak': FP64_PEAK_TFLOPS,
