@@ -88,6 +88,8 @@ class Experiment:
         self.updaters = {'accumulate': _accumulate, 'set': _set,
                          'update_field_with_exchange': self._update_field_with_exchange}
         self._exchange: Dict[Tuple, list] = {}      # device field path -> queued (location, dims, count)
+        self._ports: Dict[int, Tuple] = {}          # id(process) -> (process, its port names)
+        self._updater_cache: Dict[Tuple, str] = {}  # resolved schema updater per leaf path
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -126,6 +128,7 @@ class Experiment:
     def _register(self, path, schema):
         if not isinstance(schema, dict):
             return
+        self._updater_cache.clear()
         keys = [k for k in schema if not k.startswith('_')]
         if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
@@ -143,6 +146,12 @@ class Experiment:
             self._register(path + (k,), schema[k])
 
     def _updater_at(self, path):
+        name = self._updater_cache.get(path)
+        if name is None:
+            name = self._updater_cache[path] = self._resolve_updater(path)
+        return name
+
+    def _resolve_updater(self, path):
         if path in self.schema:
             return self.schema[path]
         for pat in self._globs:                  # '*' patterns, in registration order
@@ -151,22 +160,31 @@ class Experiment:
         return 'accumulate'
 
     # -- updates ---------------------------------------------------------------
+    def _port_names(self, proc):
+        # a process's ports_schema() is static once it is built (process.py:275-289);
+        # the entry keeps the process alive, so its id cannot be reused
+        entry = self._ports.get(id(proc))
+        if entry is None or entry[0] is not proc:
+            entry = self._ports[id(proc)] = (proc, tuple(proc.ports_schema()))
+        return entry[1]
+
     def process_states(self, path, proc):
-        return {port: self.get(self.port_path(path, port)) for port in proc.ports_schema()}
+        return {port: self.get(self.port_path(path, port)) for port in self._port_names(proc)}
 
     def apply_update(self, update, proc_path):
         for port, value in update.items():
-            self._apply(self.port_path(proc_path, port), value, proc_path)
+            path = self.port_path(proc_path, port)
+            self._apply(self.get(path[:-1]), path, value, proc_path)
 
-    def _apply(self, path, update, proc_path):
-        parent = self.get(path[:-1])
+    def _apply(self, parent, path, update, proc_path):
+        # parent = the store node holding path[-1] (branches pass their own node down)
         if path[-1] not in parent:
             return
         current = parent[path[-1]]
         inline = isinstance(update, dict) and '_updater' in update
         if isinstance(current, dict) and not inline:
             for key, value in update.items():
-                self._apply(path + (key,), value, proc_path)
+                self._apply(current, path + (key,), value, proc_path)
             return
         states = None
         if inline:
@@ -177,7 +195,7 @@ class Experiment:
                 states = {up: self.get(self.port_path(proc_path, pp)) for up, pp in mapping.items()}
         else:
             name, value = self._updater_at(path), update
-        if name != 'update_field_with_exchange':
+        if name != 'update_field_with_exchange' and self._exchange:
             self._flush(path)                        # queued exchange lands first
         parent[path[-1]] = self.updaters[name](current, value, states, path) \
             if name == 'update_field_with_exchange' else self.updaters[name](current, value, states)
