@@ -125,3 +125,36 @@ def test_gpu_kremling_avogadro_is_a_parameter(dev):
             cnt = ok.step(s0, volume_fL=vol[a], rtol=1e-13, atol=1e-16, avogadro=na)[2]
             assert np.abs(got[na][:, a] - cnt).max() <= 1
     assert (got[6.022140857e23] != got[6.02214076e23]).any()
+
+
+@pytest.mark.gpu
+def test_gpu_kremling_parameter_sets_interleaved(dev):
+    """Two colonies with different parameter sets -- one with the default
+    integer exponents (n = 2, m = 1: repeated products), one with n = 1.5
+    (the pow path) and another kgly -- stepped alternately on one stream: the
+    library's per-set device parameter copies keep them apart, and each
+    matches tight odeint on its own parameters."""
+    from lens_amd.kremling import KremlingColony
+    s0 = ok.initial_state()
+    n = 16
+    sets = [{}, {'n': 1.5, 'kgly': ok.DEFAULT_PARAMETERS['kgly'] * 1.3}]
+    cols = [KremlingColony(n, device=dev, parameters=p) for p in sets]
+    for c in cols:
+        c.set_state(np.repeat(s0[:11, None], n, axis=1))
+    for _ in range(2):
+        for c in cols:
+            c.step(1.0)
+    torch.cuda.synchronize()
+    state = s0.copy()
+    for c, p in zip(cols, sets):
+        c.check_status()
+        got = c.state.cpu().numpy()
+        params = dict(ok.DEFAULT_PARAMETERS, **p)
+        st = s0.copy()
+        for _ in range(2):
+            internal = ok.step(st, rtol=1e-13, atol=1e-16, params=params)[0]
+            st[:8] = internal
+        assert _close(got[:8, 0], st[:8]), (p, got[:8, 0], st[:8])
+        assert np.array_equal(got[:, 0], got[:, n - 1])
+    del state
+    assert not np.allclose(cols[0].state.cpu().numpy()[:8, 0], cols[1].state.cpu().numpy()[:8, 0])
