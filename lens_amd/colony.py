@@ -93,6 +93,7 @@ class Colony:
         self.h_state = z(ld)
         self.time = 0.0
         self.step_index = 0
+        self._layout = 0             # bumped when step buffers are reallocated (Colony.capture checks it)
         self.lattice: Optional[Lattice] = None
         self.router = None       # distributed.AgentRouter (row-banded multi-rank lattice colonies)
         self.ordinal = None      # global single-rank-order key (set by the router)
@@ -198,6 +199,7 @@ class Colony:
             raise ValueError('agents outside this rank\'s row band: attach a distributed.AgentRouter '
                              '(division moves daughters across band edges)')
         self.occ = occupancy(self.bin_lin, self.n)
+        self._layout += 1            # captured graphs hold the old occupancy buffers
 
     def gather_external(self):
         """external := field at the agent's bin (get_local_environments)."""
@@ -390,7 +392,10 @@ class Colony:
         side-stream overlap. A single-GPU lattice step qualifies: the pass plan
         depends only on Δt, and the uniform-plane skip is read by the kernels
         from device memory. Capture records the launches without running them,
-        so the colony state is unchanged until the first replay."""
+        so the colony state is unchanged until the first replay. The graph
+        holds the buffers and the agent count of capture time: set_agents()
+        values may change between replays (they are copied in place), but a
+        re-binning of moved agents invalidates it (replay raises)."""
         lat = self.lattice
         if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
                 (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
@@ -400,12 +405,17 @@ class Colony:
             raise ValueError('Colony.capture: steps >= 1')
         graph = torch.cuda.CUDAGraph()
         t0, s0 = self.time, self.step_index
+        layout, n = self._layout, self.n
         with torch.cuda.graph(graph):
             for _ in range(steps):
                 self.step(dt)
         self.time, self.step_index = t0, s0      # capture ran nothing
 
         def replay():
+            # the graph holds raw device pointers and the agent count of capture time
+            if self._layout != layout or self.n != n:
+                raise RuntimeError('Colony.capture: the colony was re-laid out (agents moved or counted '
+                                   'anew) after capture; capture again')
             graph.replay()
             self.time += dt * steps
             self.step_index += steps

@@ -105,3 +105,17 @@ def test_graph_replay_lattice_colony(dev):
     assert np.array_equal(eager.counts[:, :n].cpu().numpy(), graphed.counts[:, :n].cpu().numpy())
     for m in eager.lattice.molecules:
         assert np.array_equal(eager.lattice.owned(m).cpu().numpy(), graphed.lattice.owned(m).cpu().numpy()), m
+
+
+def test_graph_replay_refuses_moved_agents(dev):
+    """Moving agents re-bins them (new occupancy buffers): a graph captured
+    before holds the old ones, so its replay raises instead of scattering the
+    exchange into stale bins."""
+    col = _lattice_colony(dev, n=500, nx=64)
+    col.step(1.0)
+    replay = col.capture(1.0, 1)
+    replay()
+    rng = np.random.default_rng(9)
+    col.set_agents(location=rng.uniform(0.0, 64.0, (2, col.n)))
+    with pytest.raises(RuntimeError):
+        replay()
