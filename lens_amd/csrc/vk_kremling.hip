@@ -314,7 +314,10 @@ static int small_int(double e) {   // e as an exponent of repeated products, or 
 
 // Device copies of the parameter sets in use, created at a set's first launch
 // (synchronous copy, so a launch captured into a graph later finds it) and
-// kept for the life of the process: colonies use a handful of sets.
+// kept: colonies use a handful of sets.  A parameter scan that passes more
+// than KP_SETS_MAX distinct sets drains the device and starts the cache over
+// (no launch in flight can still read a freed copy).
+constexpr size_t KP_SETS_MAX = 4096;
 static std::mutex g_kp_mutex;
 static std::vector<std::pair<Kp, Kp *>> g_kp_sets;
 
@@ -322,6 +325,12 @@ static int device_params(const Kp &p, const Kp **out) {
     std::lock_guard<std::mutex> lock(g_kp_mutex);
     for (auto &e : g_kp_sets)
         if (memcmp(&e.first, &p, sizeof(Kp)) == 0) { *out = e.second; return VK_OK; }
+    if (g_kp_sets.size() >= KP_SETS_MAX) {
+        int rc = vk::hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(kremling params)");
+        if (rc) return rc;
+        for (auto &e : g_kp_sets) (void)hipFree(e.second);
+        g_kp_sets.clear();
+    }
     Kp *d = nullptr;
     int rc = vk::hip_check(hipMalloc(&d, sizeof(Kp)), "hipMalloc(kremling params)");
     if (rc) return rc;
