@@ -434,10 +434,16 @@ def main():
             replay()
         e_all[1].record()
     else:
+        # running attempt count after each timed step (device copies, read after timing):
+        # the per-step distribution of DP45 attempts, which falls as the colony equilibrates
+        att_hist = torch.zeros(args.steps, dtype=torch.int64, device=dev)
+        n_hist = []
         t0 = time.perf_counter()
         for k in range(args.steps):
             agent_steps += col.n
+            n_hist.append(col.n)
             one_step(timing[k])
+            att_hist[k].copy_(col.attempts)
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()
@@ -470,8 +476,13 @@ def main():
         integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
         variant = col.engine.default_variant()
         kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec', 3: 'vk_dopri5_wspec'}[variant]
+        per_step = None
+        if not use_graph:
+            cum = att_hist.cpu().numpy().astype(float)
+            per_step = [round(float(a) / n, 4) for a, n in zip(np.diff(np.concatenate([[0.0], cum])), n_hist)]
         integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / agent_steps,
+                 'dp45_attempts_per_agent_step_by_step': per_step,
                  'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),
                  'achieved_tflops': integ_flops / (kin_ms * 1e-3) / 1e12 if kin_ms else None,
                  'peak_tflops': FP64_PEAK_TFLOPS}
