@@ -89,8 +89,8 @@ def parse():
     p.add_argument('--overlap-kinetics', action='store_true',
                    help='run kinetics + gather on a side stream beside the diffusion passes')
     p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
-                   help='replay the timed steps from a captured HIP graph (auto: launch-bound steps that take '
-                        'no host decision -- no division, no lattice or a single-GPU lattice up to 2048^2: C2, C3)')
+                   help='replay the timed steps from a captured HIP graph (auto: every single-GPU step that takes '
+                        'no host decision, i.e. no division: C2, C3, C4)')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -401,18 +401,19 @@ def main():
         one_step(warm_timing[k])
     barrier()
     col.check_status()
-    # HIP-graph replay: a step that is one small kinetics launch is host-bound
-    # when issued from Python; the graph holds `per_graph` steps
-    # (auto: launch-bound steps -- no lattice (C2) or a small one (C3); the C4 step is 2 ms of
-    # GPU work and keeps its per-step kernel timings)
-    small = lat is None or (world == 1 and (lat.row_hi - lat.row_lo) * lat.ny <= 2048 * 2048)
-    use_graph = (args.graph == 'on' or (args.graph == 'auto' and small and col.cells is None)) and balancer is None
+    # HIP-graph replay of the timed steps: every step whose launch sequence takes no
+    # host decision (one GPU, no division).  A C2 step is one 4-us launch that costs
+    # 40 us to issue from Python; a C4 step measured 2.025 -> 1.886 ms replayed
+    # (profiles/r02e_graph_ab.log).  Multi-GPU steps stay eager (host-driven halo
+    # collectives).
+    use_graph = (args.graph == 'on' or (args.graph == 'auto' and world == 1 and col.cells is None)) \
+        and balancer is None
     graph_info = None
     if use_graph:
         per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
-        # the per-step attempt count (a reduction launch after each kinetics
-        # launch) is report bookkeeping, not workload: the graph leaves it out and
-        # the attempts are read from the last timed step's per-agent counts
+        # the per-step attempt count is report bookkeeping (a reduction launch after
+        # each kinetics launch, which would double a C2 step): the graph leaves it
+        # out and the attempts are read from the last timed step's per-agent counts
         col.count_attempts(False)
         replay = col.capture(1.0, per_graph)
         replay()             # uploads the graph; its steps are warmup, not timed
@@ -451,16 +452,25 @@ def main():
     copy_floor = time_copy_floor(lat) if lat is not None and world == 1 else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
-    if use_graph:           # no per-launch events inside a graph: the whole replayed step
-        kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps if lat is None else None
-    else:
-        kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
-    diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
-               if lat is not None and not use_graph else None)
-    if use_graph:            # every timed step integrates the same agents (no division): last step x steps
+    if use_graph:                     # same agents every step (no division): last step x steps
         attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
         graph_info['attempts_from'] = 'per-agent attempt counts of the last timed step x steps'
+    if use_graph and lat is None:     # the replayed step is the kinetics launch
+        kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
+        diff_ms = None
+    elif use_graph:
+        # no per-launch events inside a graph: the kinetics / diffusion split of the
+        # report comes from one eager step after the timed region
+        t_one = mk()
+        col.step(1.0, timing=t_one)
+        barrier()
+        kin_ms = t_one['kin'][0].elapsed_time(t_one['kin'][1])
+        diff_ms = t_one['diff'][0].elapsed_time(t_one['diff'][1])
+        graph_info['kernel_split_from'] = 'one eager step after the timed region'
     else:
+        kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
+        diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
+                   if lat is not None else None)
         attempts = float(col.attempts.item())
     if dist is not None:
         if args.dist_backend == 'gloo':
