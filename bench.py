@@ -393,38 +393,41 @@ def main():
 
     ev = lambda: torch.cuda.Event(enable_timing=True)
     mk = lambda: ({'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())})
-    timing = [mk() for _ in range(args.steps)]          # timed steps only
-    warm_timing = [mk() for _ in range(args.warmup)]
-    col.count_attempts(True)
+    # Per-step bookkeeping inside the timed region is kept to what cannot be had
+    # afterwards.  Lattice steps record no HIP events (the kinetics / diffusion
+    # split comes from one eager step after the timed region); the DP45 attempts
+    # are per-agent counts copied device-to-device after each step and reduced
+    # after timing (a torch reduction per step cost ~0.1 ms of a 1.9-ms C4 step).
+    timing = [mk() if lat is None else None for _ in range(args.steps)]
+    # with division the per-agent counts are reshuffled after the kinetics: the
+    # colony sums them itself, right after the launch (an 85-ms C5 step does not
+    # notice the reduction)
+    divides = col.cells is not None
+    col.count_attempts(divides)
     # warmup runs exactly the timed loop body (first-use costs land here)
     for k in range(args.warmup):
-        one_step(warm_timing[k])
+        one_step(mk() if lat is None else None)
     barrier()
     col.check_status()
     # HIP-graph replay of the timed steps: every step whose launch sequence takes no
     # host decision (one GPU, no division).  A C2 step is one 4-us launch that costs
-    # 40 us to issue from Python; a C4 step measured 2.025 -> 1.886 ms replayed
-    # (profiles/r02e_graph_ab.log).  Multi-GPU steps stay eager (host-driven halo
+    # 40 us to issue from Python.  Multi-GPU steps stay eager (host-driven halo
     # collectives).
     use_graph = (args.graph == 'on' or (args.graph == 'auto' and world == 1 and col.cells is None)) \
         and balancer is None
     graph_info = None
     if use_graph:
         per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
-        # the per-step attempt count is report bookkeeping (a reduction launch after
-        # each kinetics launch, which would double a C2 step): the graph leaves it
-        # out and the attempts are read from the last timed step's per-agent counts
-        col.count_attempts(False)
         replay = col.capture(1.0, per_graph)
         replay()             # uploads the graph; its steps are warmup, not timed
         barrier()
         col.check_status()
         graph_info = {'steps_per_graph': per_graph, 'replays': args.steps // per_graph,
                       'untimed_warmup_replay_steps': per_graph}
-    if col.attempts is not None:
-        col.attempts.zero_()
     agent_steps = 0          # agents integrated, summed over the timed steps (divisions grow n)
     n_start = col.n
+    if divides:
+        col.attempts.zero_()
     barrier()
     if use_graph:
         e_all = (ev(), ev())
@@ -435,16 +438,19 @@ def main():
             replay()
         e_all[1].record()
     else:
-        # running attempt count after each timed step (device copies, read after timing):
-        # the per-step distribution of DP45 attempts, which falls as the colony equilibrates
-        att_hist = torch.zeros(args.steps, dtype=torch.int64, device=dev)
+        ns_hist = (torch.zeros((args.steps, 1), dtype=torch.int64, device=dev) if divides else
+                   torch.zeros((args.steps, col.ld), dtype=torch.int32, device=dev))
         n_hist = []
         t0 = time.perf_counter()
         for k in range(args.steps):
-            agent_steps += col.n
-            n_hist.append(col.n)
+            n_k = col.n                   # agents integrated this step (division comes after the kinetics)
+            agent_steps += n_k
             one_step(timing[k])
-            att_hist[k].copy_(col.attempts)
+            n_hist.append(n_k)
+            if divides:
+                ns_hist[k, 0] = col.attempts      # running total (the colony's own sum)
+            else:
+                ns_hist[k, :n_k].copy_(col.nsteps[:n_k])
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()
@@ -452,26 +458,34 @@ def main():
     copy_floor = time_copy_floor(lat) if lat is not None and world == 1 else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
+    per_step = None
     if use_graph:                     # same agents every step (no division): last step x steps
         attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
         graph_info['attempts_from'] = 'per-agent attempt counts of the last timed step x steps'
-    if use_graph and lat is None:     # the replayed step is the kinetics launch
+    elif divides:
+        cum = ns_hist[:, 0].to(torch.int64).cpu().numpy().astype(float)
+        sums = np.diff(np.concatenate([[0.0], cum]))
+        attempts = float(col.attempts.item())
+        per_step = [round(a / n, 4) for a, n in zip(sums, n_hist)]
+    else:
+        sums = ns_hist.to(torch.int64).sum(dim=1).cpu().numpy().astype(float)
+        attempts = float(sums.sum())
+        per_step = [round(a / n, 4) for a, n in zip(sums, n_hist)]
+    if lat is None and use_graph:     # the replayed step is the kinetics launch
         kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
         diff_ms = None
-    elif use_graph:
-        # no per-launch events inside a graph: the kinetics / diffusion split of the
-        # report comes from one eager step after the timed region
+    elif lat is None:
+        kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
+        diff_ms = None
+    else:
+        # the kinetics / diffusion split of the report: one eager step after the timed region
         t_one = mk()
-        col.step(1.0, timing=t_one)
+        one_step(t_one)
         barrier()
         kin_ms = t_one['kin'][0].elapsed_time(t_one['kin'][1])
         diff_ms = t_one['diff'][0].elapsed_time(t_one['diff'][1])
-        graph_info['kernel_split_from'] = 'one eager step after the timed region'
-    else:
-        kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
-        diff_ms = (sum(t['diff'][0].elapsed_time(t['diff'][1]) for t in timing) / args.steps
-                   if lat is not None else None)
-        attempts = float(col.attempts.item())
+        if graph_info is not None:
+            graph_info['kernel_split_from'] = 'one eager step after the timed region'
     if dist is not None:
         if args.dist_backend == 'gloo':
             el, n_agents = el.cpu(), n_agents.cpu()
@@ -486,10 +500,6 @@ def main():
         integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
         variant = col.engine.default_variant()
         kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec', 3: 'vk_dopri5_wspec'}[variant]
-        per_step = None
-        if not use_graph:
-            cum = att_hist.cpu().numpy().astype(float)
-            per_step = [round(float(a) / n, 4) for a, n in zip(np.diff(np.concatenate([[0.0], cum])), n_hist)]
         integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / agent_steps,
                  'dp45_attempts_per_agent_step_by_step': per_step,
