@@ -395,9 +395,13 @@ def main():
     mk = lambda: ({'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())})
     # Per-step bookkeeping inside the timed region is kept to what cannot be had
     # afterwards.  Lattice steps record no HIP events (the kinetics / diffusion
-    # split comes from one eager step after the timed region); the DP45 attempts
-    # are per-agent counts copied device-to-device after each step and reduced
-    # after timing (a torch reduction per step cost ~0.1 ms of a 1.9-ms C4 step).
+    # split comes from one eager step after the timed region).  A non-dividing
+    # colony integrates the same agents every step, so its DP45 attempts are read
+    # from the last step's per-agent counts (a per-step torch reduction or device
+    # copy of the counts is a launch of its own in every step).  Eager C4 still
+    # pays a fixed ~1.5 ms per timed region that the graph does not (2.09 vs
+    # 1.93 ms per step over 10 steps, 1.91 vs 1.88 over 50;
+    # profiles/r02f_eager_vs_graph.log).
     timing = [mk() if lat is None else None for _ in range(args.steps)]
     # with division the per-agent counts are reshuffled after the kinetics: the
     # colony sums them itself, right after the launch (an 85-ms C5 step does not
@@ -438,8 +442,7 @@ def main():
             replay()
         e_all[1].record()
     else:
-        ns_hist = (torch.zeros((args.steps, 1), dtype=torch.int64, device=dev) if divides else
-                   torch.zeros((args.steps, col.ld), dtype=torch.int32, device=dev))
+        att_hist = torch.zeros(args.steps, dtype=torch.int64, device=dev) if divides else None
         n_hist = []
         t0 = time.perf_counter()
         for k in range(args.steps):
@@ -448,9 +451,7 @@ def main():
             one_step(timing[k])
             n_hist.append(n_k)
             if divides:
-                ns_hist[k, 0] = col.attempts      # running total (the colony's own sum)
-            else:
-                ns_hist[k, :n_k].copy_(col.nsteps[:n_k])
+                att_hist[k] = col.attempts        # running total (the colony's own sum)
     barrier()
     elapsed = time.perf_counter() - t0
     col.check_status()
@@ -459,18 +460,14 @@ def main():
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
     per_step = None
-    if use_graph:                     # same agents every step (no division): last step x steps
-        attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
-        graph_info['attempts_from'] = 'per-agent attempt counts of the last timed step x steps'
-    elif divides:
-        cum = ns_hist[:, 0].to(torch.int64).cpu().numpy().astype(float)
-        sums = np.diff(np.concatenate([[0.0], cum]))
+    attempts_from = 'per-agent attempt counts of the last timed step x steps'
+    if divides:
+        cum = att_hist.cpu().numpy().astype(float)
         attempts = float(col.attempts.item())
-        per_step = [round(a / n, 4) for a, n in zip(sums, n_hist)]
-    else:
-        sums = ns_hist.to(torch.int64).sum(dim=1).cpu().numpy().astype(float)
-        attempts = float(sums.sum())
-        per_step = [round(a / n, 4) for a, n in zip(sums, n_hist)]
+        per_step = [round(a / n, 4) for a, n in zip(np.diff(np.concatenate([[0.0], cum])), n_hist)]
+        attempts_from = 'colony sum after every kinetics launch'
+    else:                             # same agents every step (no division): last step x steps
+        attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
     if lat is None and use_graph:     # the replayed step is the kinetics launch
         kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
         diff_ms = None
@@ -502,7 +499,7 @@ def main():
         kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec', 3: 'vk_dopri5_wspec'}[variant]
         integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / agent_steps,
-                 'dp45_attempts_per_agent_step_by_step': per_step,
+                 'dp45_attempts_per_agent_step_by_step': per_step, 'attempts_from': attempts_from,
                  'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),
                  'achieved_tflops': integ_flops / (kin_ms * 1e-3) / 1e12 if kin_ms else None,
                  'peak_tflops': FP64_PEAK_TFLOPS}
