@@ -91,6 +91,10 @@ def parse():
     p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
                    help='replay the timed steps from a captured HIP graph (auto: every single-GPU step that takes '
                         'no host decision, i.e. no division: C2, C3, C4)')
+    p.add_argument('--settle-ms', type=float, default=30.0,
+                   help='after the W warmup steps, run more untimed steps until the warmup has kept the GPU '
+                        'busy this long (power-management transient, profiles/r02g_eager_trace_gaps.log); '
+                        'reported as untimed_settle_steps')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     return p.parse_args()
@@ -398,10 +402,8 @@ def main():
     # split comes from one eager step after the timed region).  A non-dividing
     # colony integrates the same agents every step, so its DP45 attempts are read
     # from the last step's per-agent counts (a per-step torch reduction or device
-    # copy of the counts is a launch of its own in every step).  Eager C4 still
-    # pays a fixed ~1.5 ms per timed region that the graph does not (2.09 vs
-    # 1.93 ms per step over 10 steps, 1.91 vs 1.88 over 50;
-    # profiles/r02f_eager_vs_graph.log).
+    # copy of the counts is a launch of its own in every step).  Eager vs graph
+    # C4: profiles/r02f_eager_vs_graph.log, profiles/r02g_eager_trace_gaps.log.
     timing = [mk() if lat is None else None for _ in range(args.steps)]
     # with division the per-agent counts are reshuffled after the kinetics: the
     # colony sums them itself, right after the launch (an 85-ms C5 step does not
@@ -414,17 +416,37 @@ def main():
     # (every kernel, profiles/r02g_eager_trace_gaps.log).  So it runs first.
     col.check_status()
     barrier()
-    # warmup runs exactly the timed loop body (first-use costs land here)
-    for k in range(args.warmup):
-        one_step(mk() if lat is None else None)
-    barrier()
-    col.check_status()
     # HIP-graph replay of the timed steps: every step whose launch sequence takes no
     # host decision (one GPU, no division).  A C2 step is one 4-us launch that costs
     # 40 us to issue from Python.  Multi-GPU steps stay eager (host-driven halo
     # collectives).
     use_graph = (args.graph == 'on' or (args.graph == 'auto' and world == 1 and col.cells is None)) \
         and balancer is None
+    # warmup runs exactly the timed loop body (first-use costs land here)
+    t_warm = time.perf_counter()
+    for k in range(args.warmup):
+        one_step(mk() if lat is None else None)
+    barrier()
+    # Settle: the chip runs the first ~10 ms of load after an idle spell up to
+    # 40 % slower (profiles/r02g_eager_trace_gaps.log), and W short steps (a
+    # 0.3-ms banded step at 8 GPUs) do not cover that.  More untimed steps run
+    # until the warmup has lasted --settle-ms; every rank runs the same count.
+    # Graph replay needs none: its upload replay (per_graph steps) runs just
+    # before the timed region.
+    settle_steps = 0
+    if args.settle_ms > 0 and args.warmup > 0 and not use_graph:
+        per = (time.perf_counter() - t_warm) / args.warmup
+        need = torch.tensor([max(0.0, args.settle_ms * 1e-3 - per * args.warmup) / max(per, 1e-6)],
+                            dtype=torch.float64, device=dev)
+        if dist is not None:
+            if args.dist_backend == 'gloo':
+                need = need.cpu()
+            dist.all_reduce(need, op=dist.ReduceOp.MAX)
+        settle_steps = int(min(2000, np.ceil(float(need.item()))))
+        for k in range(settle_steps):
+            one_step(mk() if lat is None else None)
+        barrier()
+    col.check_status()
     graph_info = None
     if use_graph:
         per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
@@ -568,6 +590,7 @@ def main():
         out = {
             'metric': METRIC, 'value': value, 'unit': 'agent-steps/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3,
+            'untimed_settle_steps': settle_steps,
             'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
             'data': 'synthetic (seeded heterogeneous colony, SURVEY.md §8d distributions)',
             'config': {'workload': desc, 'agents': n_total, 'lattice': [nx, nx] if nx else None,
