@@ -100,6 +100,15 @@ def parse():
     return p.parse_args()
 
 
+def settle_steps_needed(warmup_s: float, warmup_steps: int, settle_ms: float, cap: int = 2000) -> int:
+    """Untimed steps to add after `warmup_steps` steps that took `warmup_s` seconds
+    so that the warmup lasts at least `settle_ms` (at the warmup's own pace)."""
+    if settle_ms <= 0 or warmup_steps <= 0:
+        return 0
+    per = max(warmup_s / warmup_steps, 1e-6)
+    return int(min(cap, np.ceil(max(0.0, settle_ms * 1e-3 - warmup_s) / per)))
+
+
 def build_rank(args, rank, world, dev):
     """This rank's share of the workload: (colony, lattice or None, host inputs).
     ``args.agents`` (optional) overrides the agent count (tests)."""
@@ -435,14 +444,13 @@ def main():
     # before the timed region.
     settle_steps = 0
     if args.settle_ms > 0 and args.warmup > 0 and not use_graph:
-        per = (time.perf_counter() - t_warm) / args.warmup
-        need = torch.tensor([max(0.0, args.settle_ms * 1e-3 - per * args.warmup) / max(per, 1e-6)],
+        need = torch.tensor([float(settle_steps_needed(time.perf_counter() - t_warm, args.warmup, args.settle_ms))],
                             dtype=torch.float64, device=dev)
         if dist is not None:
             if args.dist_backend == 'gloo':
                 need = need.cpu()
             dist.all_reduce(need, op=dist.ReduceOp.MAX)
-        settle_steps = int(min(2000, np.ceil(float(need.item()))))
+        settle_steps = int(need.item())
         for k in range(settle_steps):
             one_step(mk() if lat is None else None)
         barrier()
