@@ -440,8 +440,7 @@ def main():
     # 40 % slower (profiles/r02g_eager_trace_gaps.log), and W short steps (a
     # 0.3-ms banded step at 8 GPUs) do not cover that.  More untimed steps run
     # until the warmup has lasted --settle-ms; every rank runs the same count.
-    # Graph replay needs none: its upload replay (per_graph steps) runs just
-    # before the timed region.
+    # With graph replay the settle replays come after the capture (below).
     settle_steps = 0
     if args.settle_ms > 0 and args.warmup > 0 and not use_graph:
         need = torch.tensor([float(settle_steps_needed(time.perf_counter() - t_warm, args.warmup, args.settle_ms))],
@@ -462,6 +461,22 @@ def main():
         replay()             # uploads the graph; its steps are warmup, not timed
         barrier()
         col.check_status()
+        if args.settle_ms > 0:
+            # the capture left the GPU idle: settle again, with replays, right
+            # before the timed region (a 10-step C3 replay lasts only 3.7 ms)
+            t_rep = time.perf_counter()
+            replay()
+            barrier()
+            need = torch.tensor([float(settle_steps_needed(time.perf_counter() - t_rep, 1, args.settle_ms))],
+                                dtype=torch.float64, device=dev)
+            if dist is not None:
+                if args.dist_backend == 'gloo':
+                    need = need.cpu()
+                dist.all_reduce(need, op=dist.ReduceOp.MAX)
+            for k in range(int(need.item())):
+                replay()
+            barrier()
+            settle_steps += (1 + int(need.item())) * per_graph
         graph_info = {'steps_per_graph': per_graph, 'replays': args.steps // per_graph,
                       'untimed_warmup_replay_steps': per_graph}
     agent_steps = 0          # agents integrated, summed over the timed steps (divisions grow n)
