@@ -33,7 +33,7 @@ def fake_exchange(src, cnt):
         bufs[2].copy_(src[:, lat.row_hi - h:lat.row_hi]); bufs[3].copy_(bufs[2])
         src[:, lat.row_hi:lat.row_hi + h].copy_(bufs[3])
 
-for _ in range(3):
+for _ in range(20):   # past the power-management transient after setup (profiles/r02g_eager_trace_gaps.log)
     lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
 torch.cuda.synchronize()
 t0 = time.perf_counter()
