@@ -1,6 +1,6 @@
 """Headline benchmark: agent-steps/s of the batched colony (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c3|c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c3|c2|c5|kremling]
 
 One "step" = one Delta t = 1 s of the whole colony: every agent's kinetics
 (adaptive DP5(4), FP64, rtol 1e-8 / atol 1e-12), the local-environment
@@ -9,6 +9,12 @@ exchange scatter.  Default workload = BASELINE config 4 (1M agents on a
 4096 x 4096 lattice, glucose + acetate), strong-scaled over N ranks by row
 bands (one process per GPU, RCCL halo exchange).  Inputs are resident in
 HBM before the timed region.  Rank 0 prints one JSON line.
+
+Untimed before the K timed steps: W warmup steps, then settle steps until
+the warmup has lasted --settle-ms.  The chip runs the first ~10 ms after an
+idle spell slower, and W short steps do not cover that.  On one GPU without
+division, the settle steps are replays of a HIP graph of the step that runs
+after the capture.  Their count is reported as untimed_settle_steps.
 """
 
 from __future__ import annotations
