@@ -216,6 +216,18 @@ int vk_set_stencil_depth(int32_t k);
  * every setting.                                                           */
 int vk_set_stencil_kernel(int32_t variant, int32_t rows);
 
+/* Arithmetic mode of vk_diffuse's fused passes.  0 (default) = bit-identical
+ * with the reference's f += coef * scipy.ndimage.convolve(f, LAP, 'reflect')
+ * (diffusion_field.py:385-394: summation order N, W, -4C, E, S, two roundings
+ * per update, delta-then-accumulate at the end of the step).  1 = tolerance
+ * mode: fma(coef, (N+S)+(E+W), (1-4coef)*C) per cell-substep (5 FP64 ops
+ * instead of 6) and a final pass that writes the new field without re-reading
+ * the step-start field; within ~1e-14 relative of mode 0 over a 100-substep
+ * step (tests/test_stencil_modes.py).  Single-substep passes and
+ * vk_diffuse_delta stay exact.  Returns the previous mode; other values only
+ * query.                                                                   */
+int vk_set_stencil_mode(int32_t mode);
+
 /* dst[map_row[i]*ld + a] = fields[map_field[i]*field_stride + bin_lin[a]]. */
 int vk_gather(const double *fields, int64_t field_stride, const int32_t *bin_lin,
               int64_t n_agents, const int32_t *map_field, const int32_t *map_row,

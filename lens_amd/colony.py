@@ -184,6 +184,8 @@ class Colony:
             names += ['cell', 'divide', 'lin_root', 'lin_depth', 'lin_path']
         if self.ordinal is not None:
             names.append('ordinal')
+        if self.env_fields is not None:
+            names.append('env_fields')      # NonSpatialEnvironment: each agent's own 1x1 field
         return names
 
     def refresh_bins(self):

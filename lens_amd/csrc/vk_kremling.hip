@@ -19,6 +19,7 @@
 #include <stddef.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -312,31 +313,74 @@ static int small_int(double e) {   // e as an exponent of repeated products, or 
     return (e >= 0.0 && e <= 8.0 && e == (double)(int)e) ? (int)e : -1;
 }
 
-// Device copies of the parameter sets in use, created at a set's first launch
-// (synchronous copy, so a launch captured into a graph later finds it) and
-// kept: colonies use a handful of sets.  A parameter scan that passes more
-// than KP_SETS_MAX distinct sets drains the device and starts the cache over
-// (no launch in flight can still read a freed copy).
+// Device copies of the parameter sets in use, one per (device, set), created
+// at a set's first launch on that device with a synchronous copy and kept:
+// colonies use a handful of sets.  The copy lives on the launch stream's
+// device (hipStreamGetDevice), so two colonies on two GPUs with the same
+// parameters get one copy each.  A launch being captured into a graph must
+// find its set already cached (capture forbids the synchronous copy: run one
+// eager step first); captured sets are pinned, since a graph keeps their
+// pointers.  A parameter scan that passes more than KP_SETS_MAX distinct sets
+// drains the device and frees the unpinned copies (no launch in flight can
+// still read a freed copy).
 constexpr size_t KP_SETS_MAX = 4096;
+struct KpEntry {
+    Kp p;
+    int device;
+    Kp *d;
+    bool pinned;   // referenced by a captured graph
+};
 static std::mutex g_kp_mutex;
-static std::vector<std::pair<Kp, Kp *>> g_kp_sets;
+static std::vector<KpEntry> g_kp_sets;
 
-static int device_params(const Kp &p, const Kp **out) {
+static int device_params(const Kp &p, hipStream_t stream, const Kp **out) {
+    int dev = 0;
+    int rc = stream ? vk::hip_check(hipStreamGetDevice(stream, &dev), "hipStreamGetDevice")
+                    : vk::hip_check(hipGetDevice(&dev), "hipGetDevice");
+    if (rc) return rc;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    rc = vk::hip_check(hipStreamIsCapturing(stream, &cap), "hipStreamIsCapturing");
+    if (rc) return rc;
+    const bool capturing = cap != hipStreamCaptureStatusNone;
     std::lock_guard<std::mutex> lock(g_kp_mutex);
     for (auto &e : g_kp_sets)
-        if (memcmp(&e.first, &p, sizeof(Kp)) == 0) { *out = e.second; return VK_OK; }
+        if (e.device == dev && memcmp(&e.p, &p, sizeof(Kp)) == 0) {
+            e.pinned |= capturing;
+            *out = e.d;
+            return VK_OK;
+        }
+    if (capturing) {
+        vk::set_error("vk_kremling_step: a parameter set seen for the first time during graph capture "
+                      "(its device copy is synchronous); run one eager step with it before capturing");
+        return VK_ERR_ARG;
+    }
+    int prev = 0;
+    rc = vk::hip_check(hipGetDevice(&prev), "hipGetDevice");
+    if (rc) return rc;
+    if (prev != dev && (rc = vk::hip_check(hipSetDevice(dev), "hipSetDevice"))) return rc;
     if (g_kp_sets.size() >= KP_SETS_MAX) {
-        int rc = vk::hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(kremling params)");
-        if (rc) return rc;
-        for (auto &e : g_kp_sets) (void)hipFree(e.second);
-        g_kp_sets.clear();
+        for (auto &e : g_kp_sets) {
+            if (e.pinned) continue;
+            if ((rc = vk::hip_check(hipSetDevice(e.device), "hipSetDevice")) ||
+                (rc = vk::hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize(kremling params)")))
+                break;
+            (void)hipFree(e.d);
+            e.d = nullptr;
+        }
+        g_kp_sets.erase(std::remove_if(g_kp_sets.begin(), g_kp_sets.end(),
+                                       [](const KpEntry &e) { return e.d == nullptr; }),
+                        g_kp_sets.end());
+        if (!rc) rc = vk::hip_check(hipSetDevice(dev), "hipSetDevice");
     }
     Kp *d = nullptr;
-    int rc = vk::hip_check(hipMalloc(&d, sizeof(Kp)), "hipMalloc(kremling params)");
+    if (!rc) rc = vk::hip_check(hipMalloc(&d, sizeof(Kp)), "hipMalloc(kremling params)");
+    if (!rc) {
+        rc = vk::hip_check(hipMemcpy(d, &p, sizeof(Kp), hipMemcpyHostToDevice), "hipMemcpy(kremling params)");
+        if (rc) (void)hipFree(d);
+    }
+    if (prev != dev) (void)hipSetDevice(prev);
     if (rc) return rc;
-    rc = vk::hip_check(hipMemcpy(d, &p, sizeof(Kp), hipMemcpyHostToDevice), "hipMemcpy(kremling params)");
-    if (rc) { (void)hipFree(d); return rc; }
-    g_kp_sets.emplace_back(p, d);
+    g_kp_sets.push_back(KpEntry{p, dev, d, false});
     *out = d;
     return VK_OK;
 }
@@ -362,7 +406,7 @@ extern "C" int vk_kremling_step(const vk_kremling_params *kp, int64_t n, int64_t
     p.n_int = small_int(kp->n);
     p.m_int = small_int(kp->m);
     const Kp *dp = nullptr;
-    int rc = device_params(p, &dp);
+    int rc = device_params(p, (hipStream_t)stream, &dp);
     if (rc) return rc;
     hipLaunchKernelGGL(k_kremling_dopri5, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, (hipStream_t)stream, dp,
                        n, ld, grid_h, n_grid, rtol, atol, max_steps, state, volume_fl, avogadro, h_state, flux,

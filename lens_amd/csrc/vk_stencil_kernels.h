@@ -205,11 +205,12 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
 // ---------------------------------------------------------------------------
 
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
-template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool STEADY, int U>
 __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                         const double *__restrict__ s, double *d,
                                         const double *g, const WtLane &L, int i, int c0, int c1,
-                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
+                                        double c4) {
     constexpr int R = U % 3;
     double2(&UP)[K] = R == 0 ? S0 : (R == 1 ? S1 : S2);
     double2(&CN)[K] = R == 0 ? S1 : (R == 1 ? S2 : S0);
@@ -220,7 +221,7 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     const int r_out = i - K;
     const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
     double2 base = make_double2(0.0, 0.0);
-    if (FINAL) {   // base row r_out arrived 3 iterations ago; fetch row r_out+3 (clamped into the chunk)
+    if (FINAL && !FAST) {   // base row r_out arrived 3 iterations ago; fetch row r_out+3 (clamped into the chunk)
         base = gp[R];
         if (L.wA || L.wB) gp[R] = wt_load<EDGE>(g, (int64_t)min(max(r_out + 3, c0), c1 - 1) * ny, L);
     }
@@ -240,13 +241,22 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
             leftB = L.lB ? cen.y : leftB;
             rightB = L.rB ? cen.y : rightB;
         }
-        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
-        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
-        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
+        double2 v;
+        if (FAST) {
+            // tolerance mode: c + coef*(N+S+E+W-4c) = fma(coef, (N+S)+(E+W), (1-4coef)*c),
+            // 5 FP64 ops per cell instead of 6 (coef holds (coef, 1-4coef) packed by the caller)
+            const double sA = (up.x + dn.x) + (leftA + rightA);
+            const double sB = (up.y + dn.y) + (leftB + rightB);
+            v = make_double2(fma(coef, sA, c4 * cen.x), fma(coef, sB, c4 * cen.y));
+        } else {
+            const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
+            const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
+            v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
+        }
         if (q + 1 < K) {
             FR[q + 1] = v;
         } else if (row_ok) {
-            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            if (FINAL && !FAST) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
             double *o = d + (int64_t)r_out * ny + L.cA;
             if (!EDGE) {
                 if (L.wA) wl_store(o, v);
@@ -258,44 +268,45 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     }
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U0, int... Us>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
                                          double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *d,
                                          const double *g, const WtLane &L, int i, int c0, int c1,
-                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
-    wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect,
-                                        bot_reflect, coef);
+                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
+                                         double c4) {
+    wl_iter<K, PD, EDGE, FINAL, FAST, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi,
+                                                  top_reflect, bot_reflect, coef, c4);
     if constexpr (sizeof...(Us) > 0)
-        wl_group<K, PD, EDGE, FINAL, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo, in_hi,
-                                                top_reflect, bot_reflect, coef);
+        wl_group<K, PD, EDGE, FINAL, FAST, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo,
+                                                          in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, int... Us>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
                                                 double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                                 const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
-                                                double coef) {
+                                                double coef, double c4) {
     const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
     const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
-#define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef
+#define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4
     int i = i0;
-    for (; i + PD <= i1 && i < s_lo; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);   // fill
-    for (; i + PD - 1 <= s_hi; i += PD) wl_group<K, PD, EDGE, FINAL, true, Us...>(WL_ARGS);          // steady
-    for (; i + PD <= i1; i += PD) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);               // drain
+    for (; i + PD <= i1 && i < s_lo; i += PD) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);   // fill
+    for (; i + PD - 1 <= s_hi; i += PD) wl_group<K, PD, EDGE, FINAL, FAST, true, Us...>(WL_ARGS);          // steady
+    for (; i + PD <= i1; i += PD) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);               // drain
     // tail: fewer than PD iterations, phases 0.. in order
-    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1, in_lo,
-                                                        in_hi, top_reflect, bot_reflect, coef)
+    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, FAST, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1,
+                                                              in_lo, in_hi, top_reflect, bot_reflect, coef, c4)
                   : void()), ...);
 #undef WL_ARGS
 }
 
-template <int K, int PD, bool EDGE, bool FINAL>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST>
 __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
-                                                double coef) {
+                                                double coef, double c4) {
     double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
 #pragma unroll
     for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
@@ -308,13 +319,16 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
     for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
 #pragma unroll
     for (int u = 0; u < 3; ++u)   // FINAL: base rows of the first 3 output rows (i0 - K + u)
-        gp[u] = FINAL && (L.wA || L.wB) ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
-                                        : make_double2(0.0, 0.0);
-    diffuse_wl_loop<K, PD, EDGE, FINAL>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L, c0, c1,
-                                    in_lo, in_hi, top_reflect, bot_reflect, coef);
+        gp[u] = FINAL && !FAST && (L.wA || L.wB)
+                    ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
+                    : make_double2(0.0, 0.0);
+    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L,
+                                              c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
-template <int K, int PD, bool FINAL>
+// FAST = tolerance mode (vk_set_stencil_mode(1)): FMA-contracted arithmetic and a
+// final pass without the base re-read; within ~1e-14 relative of the exact mode.
+template <int K, int PD, bool FINAL, bool FAST = false>
 __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *dst,
                                                 const double *f0, int64_t field_stride, int ny,
                                                 int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
@@ -351,10 +365,13 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
                       (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
                       (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
+    const double c4 = 1.0 - 4.0 * coef;      // FAST only
     if (edge)
-        diffuse_wl_body<K, PD, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        diffuse_wl_body<K, PD, true, FINAL, FAST>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef,
+                                                  c4);
     else
-        diffuse_wl_body<K, PD, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
+        diffuse_wl_body<K, PD, false, FINAL, FAST>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef,
+                                                   c4);
 }
 
 // Aliasing: the FINAL pass writes the field it also reads as the base plane
@@ -368,9 +385,9 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     src, dst, f0, field_stride, ny, out_lo, out_hi, in_lo, in_hi, top_reflect, bot_reflect, rows_per_chunk,      \
         tiles_x, chunks_y, n_fields, coef, uniform
 
-template <int K, int PD, bool FINAL>
+template <int K, int PD, bool FINAL, bool FAST = false>
 __global__ __launch_bounds__(256) void k_diffuse_wl(VK_WL_PARAMS) {
-    diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
+    diffuse_wl_tile<K, PD, FINAL, FAST>(VK_WL_ARGS);
 }
 
 // Rows per wave tile: g_stencil_rows, or (auto) by the height of the rows the

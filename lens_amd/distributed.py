@@ -277,6 +277,9 @@ def install_agents(col, names, pieces):
             out[:, :n_new] = pieces[name]
         setattr(col, name, out)
     col.n, col.ld = n_new, ld
+    if getattr(col, 'env_fields', None) is not None:
+        # NonSpatialEnvironment: agent a's field is env_fields[:, a] (stride ld)
+        col.env_bins = torch.arange(ld, dtype=torch.int32, device=col.device)
 
 
 class AgentBalancer:

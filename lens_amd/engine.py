@@ -22,13 +22,15 @@ What is batched (SURVEY.md §8 a9 + N2):
 * ``config['invoke'] = BatchedInvoke()`` turns every agent's
   ``BatchedConvenienceKinetics.next_update`` of a step into one kernel
   launch (lens_amd/invoke.py);
-* ``update_field_with_exchange`` on a device field (a torch CUDA tensor, as
-  :class:`lens_amd.process.BatchedDiffusionField` keeps them) never runs per
-  agent: the counts are queued while a step's updates are applied and
-  scattered by one agent-ordered launch (``vk_exchange_sorted``) before any
-  other update touches that field and before the derivers -- the same
-  additions in the same order, so the field is bit-identical to the
-  reference's one-agent-at-a-time updater.
+* ``update_field_with_exchange`` is :mod:`lens_amd.registry`'s device-aware
+  updater, the one that also binds into the reference's own
+  ``updater_registry``: on a device field (a
+  :class:`lens_amd.registry.DeviceField`, as
+  :class:`lens_amd.process.BatchedDiffusionField` keeps them) each agent's
+  call only queues its (bin, count) on the field, and the queue lands in one
+  agent-ordered scatter (``vk_exchange_sorted``) the first time anything reads
+  the field -- the same additions in the same order, so the field is
+  bit-identical to the reference's one-agent-at-a-time updater.
 """
 
 from __future__ import annotations
@@ -36,6 +38,8 @@ from __future__ import annotations
 from typing import Dict, List, Tuple
 
 import numpy as np
+
+from lens_amd.registry import DeviceField, make_update_field_with_exchange
 
 INFINITY = float('inf')
 N_A_LEGACY = 6.022140857e23
@@ -60,13 +64,6 @@ def _set(current, new, states):
     return new
 
 
-def _bin_site(location, n_bins, bounds):
-    """lattice_utils.py:34-40."""
-    i = int(np.floor(location[0] * n_bins[0] / bounds[0])) % n_bins[0]
-    j = int(np.floor(location[1] * n_bins[1] / bounds[1])) % n_bins[1]
-    return i, j
-
-
 class _InvokeNow:
     def __init__(self, process, interval, states):
         self.update = process.next_update(interval, states)
@@ -86,8 +83,7 @@ class Experiment:
         self._globs: List[Tuple] = []            # the schema paths holding a '*'
         self._port_paths: Dict[Tuple, Tuple] = {}
         self.updaters = {'accumulate': _accumulate, 'set': _set,
-                         'update_field_with_exchange': self._update_field_with_exchange}
-        self._exchange: Dict[Tuple, list] = {}      # device field path -> queued (location, dims, count)
+                         'update_field_with_exchange': make_update_field_with_exchange(self.avogadro)}
         self._ports: Dict[int, Tuple] = {}          # id(process) -> (process, its port names)
         self._updater_cache: Dict[Tuple, str] = {}  # resolved schema updater per leaf path
         self.local_time = 0.0
@@ -195,43 +191,15 @@ class Experiment:
                 states = {up: self.get(self.port_path(proc_path, pp)) for up, pp in mapping.items()}
         else:
             name, value = self._updater_at(path), update
-        if name != 'update_field_with_exchange' and self._exchange:
-            self._flush(path)                        # queued exchange lands first
-        parent[path[-1]] = self.updaters[name](current, value, states, path) \
-            if name == 'update_field_with_exchange' else self.updaters[name](current, value, states)
-
-    def _update_field_with_exchange(self, current, count, states, path):
-        loc = states['global']['location']
-        dims = states['dimensions']
-        if _is_device(current):
-            self._exchange.setdefault(path, []).append((loc, dims, int(count)))
-            return current
-        delta = np.zeros((dims['n_bins'][0], dims['n_bins'][1]), dtype=np.float64)
-        i, j = _bin_site(loc, dims['n_bins'], dims['bounds'])
-        binvol = (dims['depth'] * dims['bounds'][0] * dims['bounds'][1]) * 1e-15 / (dims['n_bins'][0] * dims['n_bins'][1])
-        delta[i, j] += count / (binvol * self.avogadro) * 1000.0
-        return current + delta
-
-    def _flush(self, path=None):
-        """Scatter the queued exchange counts of one device field (or all) in agent order."""
-        paths = [path] if path is not None else list(self._exchange)
-        for p in paths:
-            queued = self._exchange.pop(p, None)
-            if not queued:
-                continue
-            from lens_amd.process import scatter_exchange
-            parent = self.get(p[:-1])
-            parent[p[-1]] = scatter_exchange(parent[p[-1]], queued, self.avogadro)
+        parent[path[-1]] = self.updaters[name](current, value, states)
 
     def send_updates(self, updates, derivers=None):
         for update, path in updates:
             self.apply_update(update.get(), path)
-        self._flush()
         if derivers is None:
             derivers = [(p, s) for p, s in self._walk(self.processes, ()) if s.is_deriver()]
         for path, deriver in derivers:
             self.apply_update(deriver.next_update(0, self.process_states(path, deriver)), path)
-            self._flush()
 
     # -- Experiment.update (experiment.py:1351-1450) ---------------------------------
     def update(self, interval):
@@ -275,16 +243,14 @@ class Experiment:
         return self
 
 
-def _is_device(x) -> bool:
-    return getattr(x, 'is_cuda', False)
-
-
 def _copy_tree(t):
     if isinstance(t, dict):
         return {k: _copy_tree(v) for k, v in t.items()}
     if isinstance(t, np.ndarray):
         return t.copy()
-    if _is_device(t):
+    if isinstance(t, DeviceField):
+        return DeviceField(t.tensor.clone())
+    if getattr(t, 'is_cuda', False):
         return t.clone()
     if isinstance(t, list):
         return list(t)

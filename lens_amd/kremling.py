@@ -85,13 +85,16 @@ class KremlingColony:
 
     def step(self, timestep: float = 1.0, carry_h: bool = False):
         grid_h, n_grid = output_grid(timestep)
-        if not carry_h:
-            self.h_state.zero_()      # odeint restarts every call
-        native.check(native._lib.vk_kremling_step(
-            ctypes.byref(vk_params(self.parameters)), self.n, self.n, timestep / 3600, grid_h, n_grid,
-            self.rtol, self.atol, self.max_steps, native.ptr(self.state), native.ptr(self.volume),
-            self.avogadro, native.ptr(self.h_state), native.ptr(self.flux), native.ptr(self.counts),
-            native.ptr(self.status), native.ptr(self.nsteps), native.stream_handle()), 'vk_kremling_step')
+        # the launch stream and the parameter set's device copy (cached per
+        # device by the library) belong to this colony's GPU
+        with torch.cuda.device(self.device):
+            if not carry_h:
+                self.h_state.zero_()      # odeint restarts every call
+            native.check(native._lib.vk_kremling_step(
+                ctypes.byref(vk_params(self.parameters)), self.n, self.n, timestep / 3600, grid_h, n_grid,
+                self.rtol, self.atol, self.max_steps, native.ptr(self.state), native.ptr(self.volume),
+                self.avogadro, native.ptr(self.h_state), native.ptr(self.flux), native.ptr(self.counts),
+                native.ptr(self.status), native.ptr(self.nsteps), native.stream_handle()), 'vk_kremling_step')
 
     def check_status(self):
         st = self.status.cpu().numpy()

@@ -48,6 +48,16 @@ def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
 
 
+def stencil_mode(mode=None) -> str:
+    """Set ('exact' | 'fma') / query (None) the fused passes' arithmetic; returns the
+    previous mode.  'exact' (default) is bit-identical with the reference's
+    scipy.ndimage.convolve update; 'fma' is the tolerance mode (vk_set_stencil_mode)."""
+    native.load()
+    names = ('exact', 'fma')
+    code = -1 if mode is None else names.index(mode)
+    return names[native._lib.vk_set_stencil_mode(code)]
+
+
 class Lattice:
     def __init__(self, molecules: Sequence[str], n_bins, bounds, depth: float, diffusion: float,
                  device=None, row_band=None, halo: int = 0, avogadro: float = N_A_LEGACY,

@@ -27,7 +27,8 @@ VK_AGENT_MAX_STEPS, VK_AGENT_H_UNDERFLOW, VK_AGENT_NONFINITE = 1, 2, 4
 EXPORTS = (
     'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy', 'vk_table_specialize',
     'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_field_uniform',
-    'vk_diffuse', 'vk_diffuse_delta', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_gather', 'vk_exchange_sorted',
+    'vk_diffuse', 'vk_diffuse_delta', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_set_stencil_mode',
+    'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites', 'vk_cell_step', 'vk_divide_scratch_bytes', 'vk_divide_plan',
     'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations', 'vk_kremling_step',
     'vk_expression_step',
@@ -101,6 +102,7 @@ _SIGS = {
                           _i32, _i32, _i32, _f64, _vp, _vp], ctypes.c_int),
     'vk_set_stencil_depth': ([_i32], ctypes.c_int),
     'vk_set_stencil_kernel': ([_i32, _i32], ctypes.c_int),
+    'vk_set_stencil_mode': ([_i32], ctypes.c_int),
     'vk_gather': ([_vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp, _i64, _vp], ctypes.c_int),
     'vk_exchange_sorted': ([_vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _f64, _vp],
                            ctypes.c_int),

@@ -218,48 +218,19 @@ def _bin_sites(locations, n_bins, bounds):
     return i * n_bins[1] + j
 
 
-def scatter_exchange(field, queued, avogadro):
-    """``update_field_with_exchange`` (vivarium/core/registry.py:149-183) for every
-    queued agent of a step at once, on a device field: ``queued`` = [(location,
-    dimensions, count)] in update order.  One agent-ordered ``vk_exchange_sorted``
-    launch adds count / (bin_volume * N_A) * 1000 to each agent's bin, agent after
-    agent -- the reference's sums in the reference's order.  In place."""
-    import torch
-    from lens_amd import native
-    from lens_amd.lattice import occupancy
-    dims = queued[0][1]
-    n_bins, bounds, depth = list(dims['n_bins']), list(dims['bounds']), float(dims['depth'])
-    if any(list(q[1]['n_bins']) != n_bins or list(q[1]['bounds']) != bounds or q[1]['depth'] != depth
-           for q in queued):
-        raise ValueError('one field, one set of dimensions')
-    if tuple(field.shape) != (n_bins[0], n_bins[1]) or not field.is_contiguous():
-        raise ValueError('device field must be a contiguous [nx, ny] tensor')
-    dev = field.device
-    k = len(queued)
-    bins = torch.from_numpy(_bin_sites([q[0] for q in queued], n_bins, bounds).astype(np.int32)).to(dev)
-    counts = torch.tensor([q[2] for q in queued], dtype=torch.int64, device=dev).reshape(1, k)
-    occ_bin, occ_ptr, occ_agent = occupancy(bins, k)
-    zero = torch.zeros(1, dtype=torch.int32, device=dev)
-    binvol = (depth * bounds[0] * bounds[1]) * 1e-15 / (n_bins[0] * n_bins[1])
-    native.load()
-    native.check(native._lib.vk_exchange_sorted(
-        native.ptr(field), n_bins[0] * n_bins[1], native.ptr(occ_bin), native.ptr(occ_ptr), native.ptr(occ_agent),
-        int(occ_bin.numel()), native.ptr(counts), k, native.ptr(zero), native.ptr(zero), 1, binvol * avogadro,
-        native.stream_handle()), 'vk_exchange_sorted')
-    return field
-
-
 class BatchedDiffusionField(ProcessBase):
     """GPU drop-in for ``DiffusionField`` (vivarium/processes/diffusion_field.py:209-407).
 
     Same ``name``, ``defaults``, ``ports_schema`` and ``next_update``; the
-    fields live on the GPU (``fields`` store values are torch tensors), the
-    delta of ``diffusion_delta`` (100 / 501 / 1001 substeps for dt = 1 / 5 /
-    10 s, uniform fields skipped) comes from ``vk_diffuse_delta`` and every
-    agent's ``boundary.external`` from one gather of the pre-step fields at
-    the agents' bins.  With :class:`lens_amd.engine.Experiment` the agents'
-    ``update_field_with_exchange`` updates are scattered in one launch per
-    field (:func:`scatter_exchange`)."""
+    fields live on the GPU -- the ``fields`` store holds
+    :class:`lens_amd.registry.DeviceField` values -- the delta of
+    ``diffusion_delta`` (100 / 501 / 1001 substeps for dt = 1 / 5 / 10 s,
+    uniform fields skipped) comes from ``vk_diffuse_delta`` and every agent's
+    ``boundary.external`` from one ``vk_gather`` of the pre-step fields at the
+    agents' bins.  The agents' ``update_field_with_exchange`` updates on those
+    fields queue on the field and land in one agent-ordered launch
+    (:mod:`lens_amd.registry`, bound into the reference's updater registry or
+    :class:`lens_amd.engine.Experiment`)."""
 
     name = 'diffusion_field'
     defaults = {
@@ -289,15 +260,18 @@ class BatchedDiffusionField(ProcessBase):
                                device=self.device, avogadro=p['avogadro'])
         self.initial_agents = p['agents']
         self._torch = torch
+        nf = len(self.molecule_ids)
+        self._map = torch.arange(nf, dtype=torch.int32, device=self.device)   # plane f -> row f
 
     def ones_field(self):
         return self._torch.ones(self.n_bins, dtype=self._torch.float64, device=self.device)
 
     def _device_field(self, value):
-        t = self._torch.as_tensor(value, dtype=self._torch.float64)
-        return t.to(self.device).contiguous()
+        from lens_amd.registry import as_device_tensor
+        return as_device_tensor(value, self.device).contiguous()
 
     def ports_schema(self):
+        from lens_amd.registry import DeviceField
         local = {m: {'_default': 0.0, '_updater': 'set'} for m in self.molecule_ids}
         schema = {'agents': {}}
         for agent_id, states in self.initial_agents.items():
@@ -307,7 +281,7 @@ class BatchedDiffusionField(ProcessBase):
             'external': local}}
         init = self.parameters['initial_state']
         schema['fields'] = {
-            m: {'_value': self._device_field(init[m]) if m in init else self.ones_field(),
+            m: {'_value': DeviceField(self._device_field(init[m]) if m in init else self.ones_field()),
                 '_updater': 'accumulate', '_emit': True}
             for m in self.molecule_ids}
         schema['dimensions'] = {
@@ -315,22 +289,32 @@ class BatchedDiffusionField(ProcessBase):
         return schema
 
     def next_update(self, timestep, states):
+        from lens_amd import native
         torch = self._torch
         fields = states['fields']
         lat = self.lattice
-        for f, m in enumerate(self.molecule_ids):
-            lat.fields[f].copy_(self._device_field(fields[m]))
-        delta = lat.diffuse_delta(timestep)
-        update = {'fields': {m: delta[f] for f, m in enumerate(self.molecule_ids)}}
-        agents = states['agents']
-        if agents:
-            ids = list(agents)
-            bins = torch.from_numpy(_bin_sites([agents[a]['boundary']['location'] for a in ids], self.n_bins,
-                                               self.bounds)).to(self.device)
-            # pre-step fields at the bins (get_local_environments, diffusion_field.py:362-379)
-            vals = torch.stack([self._device_field(fields[m]).reshape(-1)[bins] for m in self.molecule_ids])
-            vals = vals.cpu().numpy()
-            update['agents'] = {
-                a: {'boundary': {'external': {m: float(vals[f, k]) for f, m in enumerate(self.molecule_ids)}}}
-                for k, a in enumerate(ids)}
+        with torch.cuda.device(self.device):
+            for f, m in enumerate(self.molecule_ids):
+                lat.fields[f].copy_(self._device_field(fields[m]))     # lands queued exchange first
+            update = {}
+            agents = states['agents']
+            if agents:
+                # pre-step fields at the agents' bins (get_local_environments,
+                # diffusion_field.py:362-379): one vk_gather, one host copy
+                ids = list(agents)
+                n = len(ids)
+                bins = torch.from_numpy(_bin_sites([agents[a]['boundary']['location'] for a in ids], self.n_bins,
+                                                   self.bounds).astype(np.int32)).to(self.device)
+                vals = torch.empty((len(self.molecule_ids), n), dtype=torch.float64, device=self.device)
+                native.check(native._lib.vk_gather(
+                    native.ptr(lat.fields), lat.field_stride, native.ptr(bins), n, native.ptr(self._map),
+                    native.ptr(self._map), int(self._map.numel()), native.ptr(vals), n, native.stream_handle()),
+                    'vk_gather')
+            delta = lat.diffuse_delta(timestep)
+            update['fields'] = {m: delta[f] for f, m in enumerate(self.molecule_ids)}
+            if agents:
+                cols = vals.cpu().numpy().T.tolist()
+                mols = self.molecule_ids
+                update['agents'] = {a: {'boundary': {'external': dict(zip(mols, col))}}
+                                    for a, col in zip(ids, cols)}
         return update

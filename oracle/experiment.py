@@ -62,12 +62,16 @@ def make_update_field_with_exchange(avogadro=N_A_LEGACY):
 
 
 class OracleExperiment:
-    def __init__(self, processes, topology, initial_state, avogadro=N_A_LEGACY):
+    def __init__(self, processes, topology, initial_state, avogadro=N_A_LEGACY, updater_registry=None):
+        """``updater_registry``: entries that replace the reference's updaters by
+        name, as a maintainer replaces one in vivarium.core.registry.updater_registry
+        (tests bind the device-aware update_field_with_exchange this way)."""
         self.processes = processes
         self.topology = topology
         self.state = _copy_tree(initial_state)
         self.updaters = {'accumulate': update_accumulate, 'set': update_set,
                          'update_field_with_exchange': make_update_field_with_exchange(avogadro)}
+        self.updaters.update(updater_registry or {})
         self.schema = {}                      # store path (with '*' globs) -> updater name
         self._globs = []                      # the schema paths holding a '*'
         self.local_time = 0.0

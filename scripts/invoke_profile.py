@@ -1,0 +1,69 @@
+"""Where the Process-API path's host time goes (lens_amd.engine.Experiment +
+BatchedInvoke + BatchedDiffusionField, scripts/invoke_throughput.py's colony):
+per-agent-step cost at several colony sizes, with and without Python's cyclic
+GC, and a cProfile of one size.
+
+    python scripts/invoke_profile.py [--profile N] [n_agents ...]
+"""
+import cProfile
+import gc
+import io
+import os
+import pstats
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from invoke_throughput import build  # noqa: E402
+
+
+def run(n, steps=3, gc_on=True, profile=False):
+    from lens_amd.engine import Experiment
+    from lens_amd.invoke import BatchedInvoke
+    dev = torch.device('cuda', 0)
+    p, t, init = build(n, dev)
+    exp = Experiment({'processes': p, 'topology': t, 'initial_state': init, 'invoke': BatchedInvoke(dev)})
+    exp.update(1.0)
+    torch.cuda.synchronize()
+    if not gc_on:
+        gc.disable()
+    prof = cProfile.Profile() if profile else None
+    t0 = time.perf_counter()
+    if prof:
+        prof.enable()
+    exp.update(float(steps))
+    torch.cuda.synchronize()
+    if prof:
+        prof.disable()
+    dt = time.perf_counter() - t0
+    gc.enable()
+    print('agents %6d  gc %-3s  %.1f us per agent-step' % (n, 'on' if gc_on else 'off', dt / (n * steps) * 1e6),
+          flush=True)
+    if prof:
+        s = io.StringIO()
+        st = pstats.Stats(prof, stream=s)
+        st.sort_stats('tottime').print_stats(25)
+        st.sort_stats('cumulative').print_stats(30)
+        print(s.getvalue(), flush=True)
+
+
+def main():
+    args = sys.argv[1:]
+    prof_n = None
+    if '--profile' in args:
+        i = args.index('--profile')
+        prof_n = int(args[i + 1])
+        del args[i:i + 2]
+    sizes = [int(x) for x in args] or [500, 2000, 8000, 32000]
+    for n in sizes:
+        run(n, gc_on=True)
+        run(n, gc_on=False)
+    if prof_n:
+        run(prof_n, profile=True)
+
+
+if __name__ == '__main__':
+    main()

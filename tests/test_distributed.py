@@ -299,3 +299,67 @@ def test_agent_balancer_evens_out_in_order(sizes):
         assert len(ords) == (r + 1) * total // world - r * total // world
         assert p0 == [o / 3.0 for o in ords]
         assert counts == [int(o / 3.0 * 1e6) - (1 << 40) for o in ords]
+
+
+class _FakeNonspatialColony(_FakeColony):
+    """A NonSpatialEnvironment colony's per-agent arrays: each agent owns a
+    column of ``env_fields`` (its 1x1 field per molecule) addressed through
+    ``env_bins`` (the balancer must move both)."""
+
+    def __init__(self, g, ld):
+        super().__init__(30, (0, 30), [0.5] * len(g), [x / 3.0 for x in g], g, ld=ld)
+        self.lattice = None
+        self.location = None
+        self.env_fields = torch.zeros((2, ld), dtype=torch.float64)
+        self.env_fields[0, :len(g)] = torch.tensor([1000.0 + x for x in g], dtype=torch.float64)
+        self.env_fields[1, :len(g)] = torch.tensor([-0.5 * x for x in g], dtype=torch.float64)
+        self.env_bins = torch.arange(ld, dtype=torch.int32)
+
+    def agent_array_names(self):
+        from lens_amd.colony import Colony
+        names = Colony.agent_array_names(self)     # the real list, env_fields included
+        return [n for n in names if hasattr(self, n)]
+
+    # attributes Colony.agent_array_names reads
+    cells = None
+    ordinal = None
+
+
+def _balance_nonspatial_worker(rank, world, port, sizes, q):
+    from lens_amd.distributed import AgentBalancer
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        start = sum(sizes[:rank])
+        g = list(range(start, start + sizes[rank]))
+        col = _FakeNonspatialColony(g, ld=len(g) + 1)
+        assert 'env_fields' in col.agent_array_names()
+        AgentBalancer(col, rank, world, tolerance=0.05).balance()
+        n = col.n
+        q.put((rank, col.ordinal[:n].tolist(), col.env_fields[:, :n].tolist(), col.env_bins.tolist(), col.ld))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_agent_balancer_moves_nonspatial_fields():
+    sizes = (5, 40, 2)
+    world = len(sizes)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_balance_nonspatial_worker, args=(r, world, port, list(sizes), q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    glob = [o for _, ords, _, _, _ in parts for o in ords]
+    assert glob == list(range(sum(sizes)))
+    for _, ords, env, bins, ld in parts:
+        assert env[0] == [1000.0 + o for o in ords]         # each agent keeps its own environment
+        assert env[1] == [-0.5 * o for o in ords]
+        assert bins == list(range(ld))                       # env_bins follows the new stride

@@ -158,3 +158,38 @@ def test_gpu_kremling_parameter_sets_interleaved(dev):
         assert np.array_equal(got[:, 0], got[:, n - 1])
     del state
     assert not np.allclose(cols[0].state.cpu().numpy()[:8, 0], cols[1].state.cpu().numpy()[:8, 0])
+
+
+@pytest.mark.gpu
+def test_gpu_kremling_graph_capture_needs_a_cached_set(dev):
+    """a parameter set's device copy is made with a synchronous
+    hipMemcpy, which graph capture forbids.  A set seen for the first time
+    while the stream captures is refused with a clear error; after one eager
+    step with it, capture works and replay equals eager stepping bit for bit."""
+    from lens_amd import native
+    from lens_amd.kremling import KremlingColony
+    s0 = ok.initial_state()
+    n = 32
+    fresh = {'kgly': ok.DEFAULT_PARAMETERS['kgly'] * 1.0001234}     # a set no other test uses
+    a = KremlingColony(n, device=dev, parameters=fresh)
+    a.set_state(np.repeat(s0[:11, None], n, axis=1))
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        g = torch.cuda.CUDAGraph()
+        with pytest.raises(native.NativeError, match='graph capture'):
+            with torch.cuda.graph(g, stream=s):
+                a.step(1.0, carry_h=True)
+    torch.cuda.synchronize()
+    b = KremlingColony(n, device=dev, parameters=fresh)
+    b.set_state(np.repeat(s0[:11, None], n, axis=1))
+    a.set_state(np.repeat(s0[:11, None], n, axis=1))
+    a.h_state.zero_()
+    a.step(1.0, carry_h=True)                 # eager: caches the set
+    b.step(1.0, carry_h=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        a.step(1.0, carry_h=True)
+    g.replay()
+    b.step(1.0, carry_h=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a.state, b.state) and torch.equal(a.counts, b.counts)

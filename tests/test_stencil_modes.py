@@ -1,0 +1,113 @@
+"""Tolerance mode of the fused stencil passes (vk_set_stencil_mode(1)).
+
+The default mode is bit-identical with the reference's
+``f += coef * scipy.ndimage.convolve(f, LAP, mode='reflect')``
+(vivarium/processes/diffusion_field.py:385-394; tests/test_gpu_parity.py).
+The tolerance mode contracts each cell-substep into
+``fma(coef, (N+S)+(E+W), (1-4coef)*C)`` and writes the final pass without the
+delta-then-accumulate re-read.  Bar: within 1e-13 relative (of the plane's
+largest value) of the scipy goldens and of the exact mode after whole steps,
+at every tile geometry; uniform planes still skipped exactly.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from oracle import cpu
+
+torch = pytest.importorskip('torch')
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden')
+TOL = 1e-13
+
+
+@pytest.fixture(scope='module')
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda', 0)
+
+
+class _mode:
+    def __init__(self, mode, depth=None, rows=None):
+        self.mode, self.depth, self.rows = mode, depth, rows
+
+    def __enter__(self):
+        from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
+        self.prev = stencil_mode(self.mode)
+        self.prev_d = stencil_depth(self.depth) if self.depth else None
+        self.prev_k = stencil_kernel(-1, self.rows) if self.rows else None
+
+    def __exit__(self, *exc):
+        from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
+        stencil_mode(self.prev)
+        if self.prev_d:
+            stencil_depth(self.prev_d)
+        if self.prev_k is not None:
+            stencil_kernel(-1, 0)
+
+
+def _rel(got, ref):
+    return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-300))
+
+
+@pytest.mark.parametrize('depth', [7, 9, 11])
+def test_fma_mode_vs_scipy_goldens(dev, depth):
+    from lens_amd.lattice import Lattice
+    z = np.load(os.path.join(GOLDEN, 'stencil.npz'))
+    with _mode('fma', depth, 16):
+        for shape in ('17x23', '64x64', '128x96'):
+            f0 = z['f0_' + shape]
+            nx, ny = f0.shape
+            for dt in (1.0, 5.0, 10.0):
+                lat = Lattice(['a', 'b'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                              initial={'a': f0, 'b': np.full((nx, ny), 2.5)})
+                lat.diffuse(dt)
+                got = lat.owned('a').cpu().numpy()
+                assert _rel(got, z['f_%s_dt%g' % (shape, dt)]) < TOL, (shape, dt)
+                assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))
+
+
+@pytest.mark.parametrize('depth,rows', [(9, 64), (7, 40), (11, 48), (9, 17)])
+@pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
+def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape):
+    from lens_amd.lattice import Lattice
+    rng = np.random.default_rng(9)
+    nx, ny = shape
+    f0 = rng.random((nx, ny)) + 0.5
+    with _mode('fma', depth, rows):
+        lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+        lat.diffuse(1.0)
+        got = lat.owned('a').cpu().numpy()
+    ref = np.ascontiguousarray(f0.copy())
+    cpu.diffuse(ref, 5.0 * 0.01, 100)
+    assert _rel(got, ref) < TOL
+    assert not np.array_equal(got, f0)
+
+
+def test_fma_mode_full_c4_planes_vs_exact_mode(dev):
+    """4096^2 x 2 fields (C4), three steps: the tolerance mode against the
+    bit-exact mode, plane by plane, and the switch back restores exactness."""
+    from lens_amd import configs
+    from lens_amd.lattice import Lattice
+    n = 4096
+    glc = configs.gaussian_bump_field((n, n))
+    ac = np.random.default_rng(2).random((n, n)) * 1e-3
+    lats = {}
+    for mode in ('exact', 'fma'):
+        with _mode(mode):
+            lat = Lattice(['glc__D_e', 'ac_e'], (n, n), (float(n), float(n)), 10.0, 5.0, device=dev,
+                          initial={'glc__D_e': glc, 'ac_e': ac})
+            for _ in range(3):
+                lat.diffuse(1.0)
+            torch.cuda.synchronize()
+            lats[mode] = lat
+    for f in range(2):
+        a = lats['exact'].fields[f]
+        b = lats['fma'].fields[f]
+        rel = float((a - b).abs().max() / a.abs().max())
+        assert rel < TOL, (f, rel)
+        assert not torch.equal(a, b)        # the modes do differ (in the last bits)
