@@ -35,6 +35,7 @@ What is batched (SURVEY.md §8 a9 + N2):
 
 from __future__ import annotations
 
+import gc
 from typing import Dict, List, Tuple
 
 import numpy as np
@@ -42,6 +43,7 @@ import numpy as np
 from lens_amd.registry import DeviceField, make_update_field_with_exchange
 
 INFINITY = float('inf')
+_MISSING = object()
 N_A_LEGACY = 6.022140857e23
 
 
@@ -86,6 +88,7 @@ class Experiment:
                          'update_field_with_exchange': make_update_field_with_exchange(self.avogadro)}
         self._ports: Dict[int, Tuple] = {}          # id(process) -> (process, its port names)
         self._updater_cache: Dict[Tuple, str] = {}  # resolved schema updater per leaf path
+        self._leaf_updaters: Dict[Tuple, Dict] = {}  # branch path -> {leaf key: updater name}
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -125,6 +128,7 @@ class Experiment:
         if not isinstance(schema, dict):
             return
         self._updater_cache.clear()
+        self._leaf_updaters.clear()
         keys = [k for k in schema if not k.startswith('_')]
         if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
@@ -170,17 +174,33 @@ class Experiment:
     def apply_update(self, update, proc_path):
         for port, value in update.items():
             path = self.port_path(proc_path, port)
-            self._apply(self.get(path[:-1]), path, value, proc_path)
+            self._apply(self.get(path[:-1]), path[:-1], path[-1], value, proc_path)
 
-    def _apply(self, parent, path, update, proc_path):
-        # parent = the store node holding path[-1] (branches pass their own node down)
-        if path[-1] not in parent:
+    def _apply(self, parent, ppath, key, update, proc_path):
+        # parent = the store node at ppath holding `key` (branches pass their own node
+        # down; leaf updater names are cached per (branch path, key), so a leaf
+        # builds no path tuple once its branch has been seen)
+        if key not in parent:
             return
-        current = parent[path[-1]]
+        current = parent[key]
         inline = isinstance(update, dict) and '_updater' in update
         if isinstance(current, dict) and not inline:
-            for key, value in update.items():
-                self._apply(current, path + (key,), value, proc_path)
+            cpath = ppath + (key,)
+            names = self._leaf_updaters.get(cpath)
+            if names is None:
+                names = self._leaf_updaters[cpath] = {}
+            updaters = self.updaters
+            for k, value in update.items():
+                cur = current.get(k, _MISSING)
+                if cur is _MISSING:
+                    continue
+                if isinstance(value, dict) or isinstance(cur, dict):     # inline updater or a branch
+                    self._apply(current, cpath, k, value, proc_path)
+                    continue
+                name = names.get(k)                                      # a plain leaf, inlined
+                if name is None:
+                    name = names[k] = self._updater_at(cpath + (k,))
+                current[k] = updaters[name](cur, value, None)
             return
         states = None
         if inline:
@@ -190,8 +210,14 @@ class Experiment:
             if mapping is not None:
                 states = {up: self.get(self.port_path(proc_path, pp)) for up, pp in mapping.items()}
         else:
-            name, value = self._updater_at(path), update
-        parent[path[-1]] = self.updaters[name](current, value, states)
+            names = self._leaf_updaters.get(ppath)
+            if names is None:
+                names = self._leaf_updaters[ppath] = {}
+            name = names.get(key)
+            if name is None:
+                name = names[key] = self._updater_at(ppath + (key,))
+            value = update
+        parent[key] = self.updaters[name](current, value, states)
 
     def send_updates(self, updates, derivers=None):
         for update, path in updates:
@@ -203,15 +229,29 @@ class Experiment:
 
     # -- Experiment.update (experiment.py:1351-1450) ---------------------------------
     def update(self, interval):
+        # Python's cyclic GC would traverse every agent's dicts over and over
+        # while a step allocates its update dicts (40 % of the loop's host time
+        # at 8k agents, scripts/invoke_profile.py): it is paused for the call;
+        # reference counting still frees everything acyclic as it goes
+        paused = gc.isenabled()
+        gc.disable()
+        try:
+            return self._update(interval)
+        finally:
+            if paused:
+                gc.enable()
+
+    def _update(self, interval):
         time = 0
         front = {}
+        # the reference re-walks the tree every iteration (:1373-1380) because a
+        # _generate / _divide update can add processes; this store applies value
+        # updates only, so the tree is fixed for the call and is walked once
+        everything = self._walk(self.processes, ())
+        processes = [(p, s) for p, s in everything if not s.is_deriver()]
+        derivers = [(p, s) for p, s in everything if s.is_deriver()]
         while time < interval:
             full_step = INFINITY
-            everything = self._walk(self.processes, ())
-            processes = [(p, s) for p, s in everything if not s.is_deriver()]
-            derivers = [(p, s) for p, s in everything if s.is_deriver()]
-            paths = {p for p, _ in processes}
-            front = {p: f for p, f in front.items() if p in paths}
             for path, proc in processes:
                 if path not in front:
                     front[path] = {'time': time, 'update': None}

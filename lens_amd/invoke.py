@@ -43,8 +43,7 @@ class _Packed:
     def __init__(self, process, interval, states):
         self.process = process
         self.interval = float(interval)
-        self.conc = np.zeros(process.table.n_species, dtype=np.float64)
-        self.m2c = process.pack_state(states, self.conc)
+        self.conc, self.m2c = process.pack_state(states)    # species values as a list, m2c
 
 
 def _run_group(items: List[_Packed], device=None) -> List[dict]:
@@ -53,7 +52,7 @@ def _run_group(items: List[_Packed], device=None) -> List[dict]:
     eng = engine_for(p0, device)
     n = len(items)
     dev = eng.device
-    conc = torch.from_numpy(np.stack([it.conc for it in items], axis=1)).to(dev).contiguous()
+    conc = torch.from_numpy(np.array([it.conc for it in items], dtype=np.float64).T.copy()).to(dev)
     params = torch.from_numpy(np.stack([it.process.param_values for it in items], axis=1)).to(dev).contiguous()
     m2c = torch.tensor([it.m2c for it in items], dtype=torch.float64, device=dev)
     delta = torch.zeros((t.n_dyn, n), dtype=torch.float64, device=dev)
@@ -72,16 +71,16 @@ def _run_group(items: List[_Packed], device=None) -> List[dict]:
             it.process._h_state = float(hv)
     else:
         raise ValueError('unknown integrator %r' % integrator)
-    flux_h = flux.cpu().numpy()
-    delta_h = delta.cpu().numpy()
-    counts_h = counts.cpu().numpy()
     st = status.cpu().numpy()
     if st.any():
         bad = int(np.flatnonzero(st)[0])
         raise FloatingPointError('agent %d: kernel status %d (1=max steps, 2=step underflow, '
                                  '4=non-finite)' % (bad, int(st[bad])))
-    return [it.process.unpack_update(flux_h[:, i], delta_h[:, i], counts_h[:, i])
-            for i, it in enumerate(items)]
+    # agent-major Python lists in one conversion each (no per-element numpy scalars)
+    flux_l = flux.t().cpu().tolist()
+    delta_l = delta.t().cpu().tolist()
+    counts_l = counts.t().cpu().tolist()
+    return [it.process.unpack_update(f, d, c) for it, f, d, c in zip(items, flux_l, delta_l, counts_l)]
 
 
 def run_batch(calls, device=None) -> List[dict]:

@@ -174,31 +174,34 @@ class BatchedConvenienceKinetics(ProcessBase):
                 'config': {'width': 1.0}}}
 
     # -- packing helpers shared with BatchedInvoke ----------------------------
-    def pack_state(self, states, conc_col: np.ndarray):
-        """Write one agent's species values into a [n_species] column."""
-        for s, (port, name) in enumerate(self.table.species):
-            v = states.get(port, {})
+    def pack_state(self, states):
+        """One agent's species values (table order) and its mmol_to_counts, as
+        Python floats."""
+        vals = []
+        for port, name in self.table.species:
+            v = states.get(port)
             v = v.get(name, 0.0) if isinstance(v, dict) else 0.0
-            conc_col[s] = float(_magnitude(v))
-        return float(_magnitude(states['global']['mmol_to_counts']))
+            vals.append(float(getattr(v, 'magnitude', v)))
+        return vals, float(_magnitude(states['global']['mmol_to_counts']))
 
-    def unpack_update(self, fluxes_col, delta_col, counts_col):
-        """Device outputs of one agent -> the reference's update dict
-        (convenience_kinetics.py:316-349)."""
+    def unpack_update(self, fluxes, deltas, counts):
+        """Device outputs of one agent (sequences in table order) -> the
+        reference's update dict (convenience_kinetics.py:316-349).  The inline
+        ``_updater`` spec of the exchange is one shared, read-only dict."""
         t = self.table
+        spec = self.__dict__.get('_exchange_spec')
+        if spec is None:
+            spec = self._exchange_spec = {
+                'updater': 'update_field_with_exchange',
+                'port_mapping': {'global': 'global', 'dimensions': 'dimensions'}}
+            self._dyn_keys = t.species[:t.n_dyn]
         update = {port: {} for port in self.port_ids}
-        update['fluxes'] = {rid: np.float64(fluxes_col[r]) for r, rid in enumerate(t.reaction_ids)}
-        for s in range(t.n_dyn):
-            port, name = t.species[s]
-            update.setdefault(port, {})[name] = float(delta_col[s])
-        for e, mol in enumerate(t.external_ids):
-            update['fields'][mol] = {
-                '_value': int(counts_col[e]),
-                '_updater': {
-                    'updater': 'update_field_with_exchange',
-                    'port_mapping': {'global': 'global', 'dimensions': 'dimensions'},
-                },
-            }
+        update['fluxes'] = dict(zip(t.reaction_ids, map(np.float64, fluxes)))
+        for (port, name), d in zip(self._dyn_keys, deltas):
+            update.setdefault(port, {})[name] = d
+        fields = update['fields']
+        for mol, c in zip(t.external_ids, counts):
+            fields[mol] = {'_value': c, '_updater': spec}
         return update
 
     def next_update(self, timestep, states):
