@@ -61,8 +61,10 @@ N_SIMDS = 256 * 4          # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 KREMLING_NY = 15
 
 
-def stencil_kernel_name(variant, depth):
+def stencil_kernel_name(variant, depth, mode='exact'):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
+    if mode == 'fma' and depth in (7, 9, 11):
+        return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
     if variant == 0:
         return 'k_diffuse_tb<%d>' % depth
     if variant == 6:
@@ -81,12 +83,17 @@ def parse():
                    help='halo depth = substeps per halo exchange (multi-GPU; default min(100, band rows): '
                         'one exchange per step; scripts/halo_sweep.py, profiles/r02_halo_sweep/)')
     p.add_argument('--exchange', default='sorted', choices=['sorted', 'atomic'])
+    p.add_argument('--no-sort-agents', dest='sort_agents', action='store_false',
+                   help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
     p.add_argument('--stencil-kernel', type=int, default=6,
                    help='0 workgroup/LDS, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows, '
                         '6 = 3 with streaming stores (default)')
     p.add_argument('--stencil-depth', type=int, default=9)
+    p.add_argument('--stencil-mode', default='fma', choices=['fma', 'exact'],
+                   help='fma (default): tolerance mode, FMA-contracted passes within 1e-13 of the exact mode '
+                        '(tests/test_stencil_modes.py); exact: bit-identical with scipy.ndimage.convolve')
     p.add_argument('--stencil-rows', type=int, default=None,
                    help='output rows per wave tile (default: 64 for C4 on one GPU, else 0 = auto by band height '
                         'and wave count)')
@@ -151,6 +158,11 @@ def build_rank(args, rank, world, dev):
                  capacity=int(n_local * 1.05) + 64 if cells is not None else None)
     col.overlap_kinetics = bool(getattr(args, 'overlap_kinetics', False))
     col.set_agents(params=params, conc=conc, location=loc if nx else None)
+    if nx and getattr(args, 'sort_agents', False):
+        # agents stored in bin order: the exchange and the gather stream (Colony.sort_by_bin);
+        # the host copies follow, for the CPU baseline
+        order = col.sort_by_bin().cpu().numpy()
+        params, conc, loc = params[:, order], conc[:, order], loc[:, order]
     if cells is not None:
         # a colony spread over one generation: divisions every step from the start
         col.set_cell_mass(rng.uniform(1339.0, 2.4 * 1100.0, n_local))
@@ -383,8 +395,9 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
         return
-    from lens_amd.lattice import stencil_depth, stencil_kernel
+    from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
     stencil_depth(args.stencil_depth)
+    stencil_mode(args.stencil_mode)
     if args.stencil_rows is None:   # 64-row tiles on the whole 4096^2 plane, else the auto rule (chunk_rows)
         args.stencil_rows = 64 if (world == 1 and args.workload == 'c4') else 0
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
@@ -435,8 +448,11 @@ def main():
     # host decision (one GPU, no division).  A C2 step is one 4-us launch that costs
     # 40 us to issue from Python.  Multi-GPU steps stay eager (host-driven halo
     # collectives).
-    use_graph = (args.graph == 'on' or (args.graph == 'auto' and world == 1 and col.cells is None)) \
-        and balancer is None
+    # Multi-GPU: an agent shard without a lattice (C2) has no per-step collective and
+    # replays like one GPU; a row band replays the launch sequences between its
+    # collectives (Colony.capture_banded), which stay eager.
+    banded = lat is not None and world > 1
+    use_graph = (args.graph == 'on' or (args.graph == 'auto' and col.cells is None)) and balancer is None
     # warmup runs exactly the timed loop body (first-use costs land here)
     t_warm = time.perf_counter()
     for k in range(args.warmup):
@@ -448,7 +464,7 @@ def main():
     # until the warmup has lasted --settle-ms; every rank runs the same count.
     # With graph replay the settle replays come after the capture (below).
     settle_steps = 0
-    if args.settle_ms > 0 and args.warmup > 0 and not use_graph:
+    if args.settle_ms > 0 and args.warmup > 0 and (not use_graph or banded):
         need = torch.tensor([float(settle_steps_needed(time.perf_counter() - t_warm, args.warmup, args.settle_ms))],
                             dtype=torch.float64, device=dev)
         if dist is not None:
@@ -461,7 +477,16 @@ def main():
         barrier()
     col.check_status()
     graph_info = None
-    if use_graph:
+    if use_graph and banded:
+        banded_step = col.capture_banded(1.0, halo_ex, allred)
+        banded_step()                        # first replay of the segment graphs: warmup, not timed
+        barrier()
+        col.check_status()
+        settle_steps += 1
+        graph_info = {'mode': 'row-band segments: [kinetics + gather + uniform probe] and one graph per halo '
+                              'block replayed, halo exchange and uniform all-reduce eager',
+                      'graphs_per_step': 1 + len(banded_step.graphs[1])}
+    elif use_graph:
         per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
         replay = col.capture(1.0, per_graph)
         replay()             # uploads the graph; its steps are warmup, not timed
@@ -490,7 +515,12 @@ def main():
     if divides:
         col.attempts.zero_()
     barrier()
-    if use_graph:
+    if use_graph and banded:
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            agent_steps += col.n
+            banded_step()
+    elif use_graph:
         e_all = (ev(), ev())
         t0 = time.perf_counter()
         e_all[0].record()
@@ -513,6 +543,11 @@ def main():
     elapsed = time.perf_counter() - t0
     col.check_status()
     stencil_pass_ms = time_stencil_pass(lat, args.stencil_depth) if lat is not None else None
+    exact_pass_ms = None
+    if lat is not None and args.stencil_mode != 'exact':
+        stencil_mode('exact')             # the bit-exact pass on the same planes, for comparison
+        exact_pass_ms = time_stencil_pass(lat, args.stencil_depth)
+        stencil_mode(args.stencil_mode)
     copy_floor = time_copy_floor(lat) if lat is not None and world == 1 else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     n_agents = torch.tensor([float(agent_steps)], dtype=torch.float64, device=dev)
@@ -525,7 +560,30 @@ def main():
         attempts_from = 'colony sum after every kinetics launch'
     else:                             # same agents every step (no division): last step x steps
         attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
-    if lat is None and use_graph:     # the replayed step is the kinetics launch
+    split = None
+    if use_graph and not banded:
+        # kernel times of the replayed step: a graph of the same steps with HIP events
+        # recorded inside it (external event nodes), replayed after the timed region
+        try:
+            replay_t = col.capture(1.0, per_graph, timing=True)
+            replay_t()
+            replay_t()
+            barrier()
+            marks = replay_t.timing
+            split = {'step_kernels_ms': float(np.mean([m['step'][0].elapsed_time(m['step'][1]) for m in marks])),
+                     'kin_ms': float(np.mean([m['kin'][0].elapsed_time(m['kin'][1]) for m in marks])),
+                     'diff_ms': float(np.mean([m['diff'][0].elapsed_time(m['diff'][1]) for m in marks]))
+                     if lat is not None else None,
+                     'from': 'HIP events inside a captured graph of %d steps, replayed after the timed region'
+                             % per_graph}
+        except Exception as exc:            # pragma: no cover - reported, then the eager fallback
+            split = {'error': repr(exc)}
+    if split is not None and 'kin_ms' in split:
+        kin_ms, diff_ms = split['kin_ms'], split['diff_ms']
+        if graph_info is not None:
+            graph_info['kernel_split_from'] = split['from']
+            graph_info['step_kernels_ms'] = split['step_kernels_ms']
+    elif lat is None and use_graph:     # the replayed step is the kinetics launch
         kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
         diff_ms = None
     elif lat is None:
@@ -540,6 +598,8 @@ def main():
         diff_ms = t_one['diff'][0].elapsed_time(t_one['diff'][1])
         if graph_info is not None:
             graph_info['kernel_split_from'] = 'one eager step after the timed region'
+            if split is not None:
+                graph_info['graph_timing_error'] = split.get('error')
     if dist is not None:
         if args.dist_backend == 'gloo':
             el, n_agents = el.cpu(), n_agents.cpu()
@@ -585,8 +645,9 @@ def main():
                 with open(pmc) as f:
                     rec = json.load(f)
                 # the committed PMC pass must describe this exact launch geometry
-                if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant')) == (
-                        depth, args.stencil_rows, cells, args.stencil_kernel):
+                if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant'),
+                        rec.get('mode', 'exact')) == (depth, args.stencil_rows, cells, args.stencil_kernel,
+                                                      args.stencil_mode):
                     traffic = rec.get('hbm_bytes_per_launch')
                     if rec.get('valu_insts_per_launch') and rec.get('clock_ghz'):
                         # the pass against the VALU-issue bound: one wave64 VALU instruction
@@ -596,7 +657,7 @@ def main():
                         valu = {'insts_per_launch': rec['valu_insts_per_launch'], 'clock_ghz': rec['clock_ghz'],
                                 'issue_bound_ms': issue_s * 1e3, 'frac': issue_s / (launch_ms * 1e-3),
                                 'busy_counter': rec.get('valu_busy_per_simd')}
-            kname = stencil_kernel_name(args.stencil_kernel, depth)
+            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode)
             roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
                         'traffic': traffic, 'bytes_per_launch': bytes_per_launch,
@@ -604,7 +665,10 @@ def main():
                         'effective_stencil_gbps': bytes_per_launch * depth / (launch_ms * 1e-3) / 1e9,
                         'fp64_tflops': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12,
                         'fp64_frac': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-                        'valu_issue': valu, 'step_diffusion_ms': diff_ms}
+                        'valu_issue': valu, 'step_diffusion_ms': diff_ms, 'stencil_mode': args.stencil_mode,
+                        'exact_mode_avg_launch_ms': exact_pass_ms,
+                        'exact_mode_frac': (bytes_per_launch / (exact_pass_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS
+                                            if exact_pass_ms else None)}
             if copy_floor is not None:
                 # the pass against the HBM rate this box delivers to a plain streaming copy of
                 # the same planes (8 TB/s is the spec; a copy reaches ~5.5)
@@ -628,6 +692,8 @@ def main():
                        'substeps_per_step': n_substeps(1.0) if nx else 0,
                        'integrator': args.integrator, 'rtol': col.rtol, 'atol': col.atol,
                        'exchange': args.exchange, 'parallelism': 'row-bands x%d' % world,
+                       'agents_in_bin_order': bool(nx and args.sort_agents),
+                       'stencil_mode': args.stencil_mode if nx else None,
                        'halo': (col.lattice.halo if col.lattice is not None else 0) if world > 1 else 0},
             'roofline': roofline,
             'integrator': integ,

@@ -203,6 +203,35 @@ class Colony:
         self.occ = occupancy(self.bin_lin, self.n)
         self._layout += 1            # captured graphs hold the old occupancy buffers
 
+    def sort_by_bin(self):
+        """Store the agents in bin order (a stable sort: agents sharing a bin keep
+        their relative order), so that the exchange scatter and the gather read
+        the per-agent arrays and the lattice as streams instead of scattered
+        lines.  Every result is unchanged: the exchange adds a bin's agents in
+        the same order (the reference's agent order), and agents do not
+        interact otherwise.  ``self.agent_order[k]`` is the index (in the
+        layout before the first sort) of the agent now stored in column k.
+        Re-sort after agents move.  Colonies whose agent order is itself a
+        result -- division appends daughters in mother order, a row band's
+        router keeps the single-rank order -- keep their layout."""
+        if self.lattice is None:
+            raise ValueError('sort_by_bin: a lattice colony')
+        if self.cells is not None or self.router is not None:
+            raise ValueError('sort_by_bin: division and routed bands keep the reference agent order')
+        n = self.n
+        perm = torch.sort(self.bin_lin[:n].to(torch.int64), stable=True).indices
+        for name in self.agent_array_names() + ['bin_lin', 'bin_ix']:
+            t = getattr(self, name)
+            if t.dim() == 1:
+                t[:n] = t[:n][perm]
+            else:
+                t[:, :n] = t[:, :n][:, perm]
+        prev = getattr(self, 'agent_order', None)
+        self.agent_order = perm if prev is None else prev[perm]
+        self.occ = occupancy(self.bin_lin, n)
+        self._layout += 1            # captured graphs hold the old occupancy buffers
+        return self.agent_order
+
     def gather_external(self):
         """external := field at the agent's bin (get_local_environments)."""
         self.lattice.gather(self.bin_lin, self.n, self.map_gather_field, self.map_gather_row, self.conc)
@@ -237,7 +266,7 @@ class Colony:
     def step(self, dt: float = 1.0, halo_exchange=None, allreduce=None, timing=None):
         """One timestep.  ``timing`` (optional) = {'kin': (ev0, ev1), 'diff': (ev0, ev1)}
         of torch.cuda.Events recorded on the launch stream around those kernels."""
-        timing = timing or {}
+        timing = {k: v for k, v in (timing or {}).items() if v is not None}
         if self.lattice is not None and self.overlap_kinetics:
             # kinetics + gather read only the pre-step field and agent state, so
             # they run on a side stream beside the diffusion passes; the pass
@@ -381,7 +410,7 @@ class Colony:
                 lat.exchange_atomic(self.bin_lin, self.n, self.counts, self.map_exch_count,
                                     self.map_exch_field)
 
-    def capture(self, dt: float = 1.0, steps: int = 1):
+    def capture(self, dt: float = 1.0, steps: int = 1, timing: bool = False):
         """Capture ``steps`` timesteps into one HIP graph (torch.cuda.CUDAGraph)
         and return a function that replays them.
 
@@ -397,20 +426,37 @@ class Colony:
         so the colony state is unchanged until the first replay. The graph
         holds the buffers and the agent count of capture time: set_agents()
         values may change between replays (they are copied in place), but a
-        re-binning of moved agents invalidates it (replay raises)."""
+        re-binning of moved agents invalidates it (replay raises).
+
+        ``timing=True`` also records HIP events inside the graph (external
+        event-record nodes, :class:`lens_amd.graph_events.GraphEvent`) around every captured step, its kinetics launch
+        and its diffusion passes: ``replay.timing`` is the list of per-step
+        ``{'step', 'kin', 'diff'}`` event pairs, holding the last replay's
+        kernel times."""
         lat = self.lattice
         if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
                 (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
             raise ValueError('Colony.capture: division, row bands, NonSpatialEnvironment and side-stream overlap '
-                             'take host decisions per step and cannot be replayed from a graph')
+                             'take host decisions per step and cannot be replayed from one graph (a row band: '
+                             'capture_banded)')
         if steps < 1:
             raise ValueError('Colony.capture: steps >= 1')
         graph = torch.cuda.CUDAGraph()
         t0, s0 = self.time, self.step_index
         layout, n = self._layout, self.n
+        marks = None
+        if timing:
+            from lens_amd.graph_events import GraphEvent     # torch refuses external events on ROCm
+            ev = GraphEvent
+            marks = [{'step': (ev(), ev()), 'kin': (ev(), ev()),
+                      'diff': (ev(), ev()) if lat is not None else None} for _ in range(steps)]
         with torch.cuda.graph(graph):
-            for _ in range(steps):
-                self.step(dt)
+            for k in range(steps):
+                if marks:
+                    marks[k]['step'][0].record()
+                self.step(dt, timing=marks[k] if marks else None)
+                if marks:
+                    marks[k]['step'][1].record()
         self.time, self.step_index = t0, s0      # capture ran nothing
 
         def replay():
@@ -423,7 +469,82 @@ class Colony:
             self.step_index += steps
 
         replay.graph = graph      # keep the graph (and its memory pool) alive with the replayer
+        replay.timing = marks
         return replay
+
+    def capture_banded(self, dt: float = 1.0, halo_exchange=None, allreduce=None):
+        """Row-banded lattice colony (multi-GPU): capture each step's launch
+        sequences between its collectives as HIP graphs and return a function
+        that runs one step -- the collectives (halo exchange, the uniform-plane
+        all-reduce) are issued eagerly, everything else is replayed.
+
+        One step of :meth:`step` on a band is, in stream order: kinetics and the
+        gather (while the first halo exchange runs on the communication
+        stream), the uniform-plane probe, its all-reduce, then per halo block a
+        halo exchange (the first one already done) and the block's fused
+        passes, and the exchange scatter after the last block.  The segments
+        between the collectives become graphs: [kinetics + gather + probe],
+        then one graph per halo block (the last with the scatter).  The
+        kernels and their arguments are the eager step's, so the results are
+        bit-identical (tests/test_distributed_gpu.py).  As with :meth:`capture`,
+        re-binned agents invalidate the graphs."""
+        from lens_amd.lattice import n_substeps
+        lat = self.lattice
+        if lat is None or not (lat.pad_top or lat.pad_bot):
+            raise ValueError('Colony.capture_banded: a row-banded lattice colony (use capture() otherwise)')
+        if self.cells is not None or self.overlap_kinetics:
+            raise ValueError('Colony.capture_banded: division and side-stream overlap take host decisions per step')
+        if halo_exchange is None:
+            raise ValueError('Colony.capture_banded: a row band needs its halo_exchange callback')
+        n_sub = n_substeps(dt, lat.diffusion_dt)
+        coeff_dt = lat.diffusion * min(dt, lat.diffusion_dt)
+        lo_min = lat.row_lo if lat.edge_top else 0
+        hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
+        blocks, j = [], 0
+        while j < n_sub:
+            cnt = min(lat.halo, n_sub - j)
+            blocks.append((j, cnt))
+            j += cnt
+        layout, n = self._layout, self.n
+        t0, s0 = self.time, self.step_index
+        g_kin = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_kin):
+            self.kinetics(dt)
+            self.gather_external()                       # pre-step field (one-step lag)
+            lat.uniform_summary(None)                    # the probe; its all-reduce is eager
+        g_blocks = []
+        for b, (j, cnt) in enumerate(blocks):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                lat._run_block(j, cnt, n_sub, coeff_dt, lat.uniform, lo_min, hi_max)
+                if b == len(blocks) - 1:
+                    self._step_exchange()
+            g_blocks.append(g)
+        self.time, self.step_index = t0, s0             # capture ran nothing
+
+        def step():
+            if self._layout != layout or self.n != n:
+                raise RuntimeError('Colony.capture_banded: the colony was re-laid out after capture; capture again')
+            main = torch.cuda.current_stream(self.device)
+            halo_done = None
+            if self.overlap_halo and self._comm_stream is not None:
+                halo_done = lat.exchange_first_halo(dt, halo_exchange, self._comm_stream)
+            g_kin.replay()
+            if allreduce is not None:
+                allreduce(lat.uniform)
+            if halo_done is not None:
+                main.wait_event(halo_done)
+            else:
+                halo_exchange(lat.state_buffer(0), blocks[0][1])
+            for b, (j, cnt) in enumerate(blocks):
+                if b:
+                    halo_exchange(lat.state_buffer(j), cnt)
+                g_blocks[b].replay()
+            self.time += dt
+            self.step_index += 1
+
+        step.graphs = (g_kin, g_blocks)
+        return step
 
     def _finish_step(self, dt):
         if self.cells is not None:

@@ -2,6 +2,7 @@
 profiles/pmc_stencil.json, which bench.py reads for roofline.traffic.
 
     python scripts/pmc_to_json.py KERNEL CELLS DEPTH ROWS VARIANT fetch.csv write.csv [out.json] [--sq sq.csv]
+                                  [--mode exact|fma]
 
 --sq: a pass with SQ_INSTS_VALU and GRBM_GUI_ACTIVE adds the VALU instructions
 per launch and the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / wall), from
@@ -33,6 +34,11 @@ def mean_counter(path, kernel, counter):
 
 
 argv = list(sys.argv[1:])
+mode = 'exact'
+if '--mode' in argv:
+    i = argv.index('--mode')
+    mode = argv[i + 1]
+    del argv[i:i + 2]
 sq = None
 if '--sq' in argv:
     i = argv.index('--sq')
@@ -44,6 +50,7 @@ fetch_kib, nf = mean_counter(fcsv, kernel, 'FETCH_SIZE')
 write_kib, nw = mean_counter(wcsv, kernel, 'WRITE_SIZE')
 rec = {
     'kernel': kernel, 'cells': int(cells), 'depth': int(depth), 'rows': int(rows), 'variant': int(variant),
+    'mode': mode,
     'fetch_size_kib': fetch_kib, 'write_size_kib': write_kib, 'dispatches': [nf, nw],
     'read_bytes_per_launch': 2.0 * fetch_kib * 1024.0,
     'write_bytes_per_launch': write_kib * 1024.0,

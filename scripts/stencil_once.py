@@ -12,6 +12,8 @@ lat = Lattice(['glc__D_e', 'ac_e'], (n, n), (float(n), float(n)), 10.0, 5.0, dev
 stencil_depth(depth)
 from lens_amd.lattice import stencil_kernel
 stencil_kernel(int(os.environ.get('VARIANT', '1')), int(os.environ.get('ROWS', '128')))
+from lens_amd.lattice import stencil_mode
+stencil_mode(os.environ.get('MODE', 'exact'))
 for _ in range(reps):
     lat.diffuse(1.0)
 torch.cuda.synchronize()

@@ -55,9 +55,10 @@ def dev():
     return torch.device('cuda', 0)
 
 
-def _args(workload, integrator='dopri5', agents=None):
+def _args(workload, integrator='dopri5', agents=None, sort_agents=False):
     return types.SimpleNamespace(workload=workload, integrator=integrator, halo=0, exchange='sorted',
-                                 generic_kernel=False, agents=agents, overlap_kinetics=False)
+                                 generic_kernel=False, agents=agents, overlap_kinetics=False,
+                                 sort_agents=sort_agents)
 
 
 def _pull(col, lat=None):
@@ -134,10 +135,28 @@ def _oracle_lattice(col, lat, fields, bins, counts):
     return out, diffused
 
 
-def _check_counts(got, ref):
+# Exchange-count flips (DP45 only; Euler counts are bit-exact).  A count is
+# int(coeff * flux_integral * mmol_to_counts), truncated toward zero
+# (convenience_kinetics.py:331).  The GPU's DP45 and the C oracle's agree to
+# ~1e-12..1e-9 relative (different division/pow rounding steers the step
+# control), so a count whose exact value lies within that distance of an
+# integer can truncate to the neighbouring integer: a one-count flip, never
+# more.  The observed flips per check are logged (VK_FLIPS_LOG) and the bound
+# below is the observed maximum with headroom (profiles/r03_count_flips.json).
+FLIP_BOUND_PER_MILLION = 20
+
+
+def _check_counts(got, ref, where=''):
     d = got.astype(np.int64) - ref.astype(np.int64)
+    flips = int(np.count_nonzero(d))
+    log = os.environ.get('VK_FLIPS_LOG')
+    if log:
+        import json
+        with open(log, 'a') as f:
+            f.write(json.dumps({'where': where, 'counts': int(d.size), 'flips': flips,
+                                'max_abs': int(np.abs(d).max()) if d.size else 0}) + '\n')
     assert np.abs(d).max() <= 1
-    assert np.count_nonzero(d) <= max(3, 1e-4 * d.size), np.count_nonzero(d)
+    assert flips <= max(2, FLIP_BOUND_PER_MILLION * 1e-6 * d.size), flips
 
 
 def _check_lattice_step(col, lat, pre, post, integrator, ref_counts):
@@ -154,7 +173,7 @@ def _check_lattice_step(col, lat, pre, post, integrator, ref_counts):
     if integrator == 'euler':
         assert np.array_equal(post.counts, ref_counts)
     else:
-        _check_counts(post.counts, ref_counts)
+        _check_counts(post.counts, ref_counts, 'lattice %dx%d' % tuple(lat.n_bins))
     new, diffused = _oracle_lattice(col, lat, pre.fields, bins, post.counts)
     for f, mol in enumerate(lat.molecules):
         assert np.array_equal(post.fields[f], new[f]), mol
@@ -171,9 +190,13 @@ def _check_lattice_step(col, lat, pre, post, integrator, ref_counts):
 # C4: 1M agents + 4096 x 4096 x 2 fields, one full step
 # ---------------------------------------------------------------------------
 
-@pytest.mark.parametrize('integrator', ['euler', 'dopri5'])
-def test_c4_full_step_vs_c_oracle(dev, integrator):
-    col, lat, _ = bench.build_rank(_args('c4', integrator), 0, 1, dev)
+@pytest.mark.parametrize('integrator,sort_agents', [('euler', False), ('dopri5', False), ('euler', True)])
+def test_c4_full_step_vs_c_oracle(dev, integrator, sort_agents):
+    """One full C4 step against the C oracle (the bench runs the agents in bin
+    order: Colony.sort_by_bin, the same results in another layout)."""
+    col, lat, _ = bench.build_rank(_args('c4', integrator, sort_agents=sort_agents), 0, 1, dev)
+    if sort_agents:
+        assert bool((col.bin_lin[1:col.n] >= col.bin_lin[:col.n - 1]).all())
     assert col.n == 1_000_000 and lat.n_bins == [4096, 4096] and len(lat.molecules) == 2
     pre = _pull(col, lat)
     col.step(1.0)
@@ -248,7 +271,7 @@ def test_c2_hundred_steps_every_agent_vs_c_oracle(dev):
         post = _pull(col)
         conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, 'dopri5', pre)
         _rel_close(post.conc[:nd], conc[:nd], 1e-9)
-        _check_counts(post.counts, counts)
+        _check_counts(post.counts, counts, 'c2 step %d' % step)
         assert np.array_equal(post.conc[nd:], pre.conc[nd:])        # held externals / enzymes
     col.check_status()
 
@@ -337,7 +360,7 @@ def test_c5_twenty_steps_vs_oracles(dev):
         _rel_close(post.conc[:nd], conc[:nd, order], 1e-9)
         assert np.array_equal(post.params, pre.params[:, order])
         assert np.array_equal(post.conc[nd:], pre.conc[nd:, order])
-        _check_counts(post.counts, counts[:, order])
+        _check_counts(post.counts, counts[:, order], 'c5 step %d' % step)
         _rel_close(post.h, h[order], 1e-3, frac=1e-2, north_star=False)
     assert divisions >= 20, divisions
 

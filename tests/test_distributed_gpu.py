@@ -357,3 +357,123 @@ def test_banded_multirate_run_equals_single_rank(world, halo, integrator):
         fields = np.concatenate([hist[i][1] for _, hist in parts], axis=1)
         assert np.array_equal(conc, ref[i][0]), i
         assert np.array_equal(fields, ref[i][1]), i
+
+
+# ---------------------------------------------------------------------------
+# HIP-graph replay on multi-rank steps: row bands (sub-graphs between the
+# collectives) and agent shards without a per-step collective (C2)
+# ---------------------------------------------------------------------------
+
+GSTEPS = 6
+
+
+def _graph_worker(rank, world, port, halo, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from lens_amd.distributed import row_bands, make_halo_exchange, make_uniform_allreduce
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        band = row_bands(NX, world)[rank]
+        eager, lat_e = _run_colony(dev, band, halo, 'dopri5')
+        graphed, lat_g = _run_colony(dev, band, halo, 'dopri5')
+        ex_e, ex_g = make_halo_exchange(lat_e, rank, world), make_halo_exchange(lat_g, rank, world)
+        ar = make_uniform_allreduce()
+        eager.step(1.0, halo_exchange=ex_e, allreduce=ar)        # first use of every kernel
+        graphed.step(1.0, halo_exchange=ex_g, allreduce=ar)
+        step = graphed.capture_banded(1.0, ex_g, ar)
+        same = []
+        for _ in range(GSTEPS):
+            eager.step(1.0, halo_exchange=ex_e, allreduce=ar)
+            step()
+            torch.cuda.synchronize()
+            n = eager.n
+            same.append(bool(torch.equal(eager.conc[:, :n], graphed.conc[:, :n]) and
+                             torch.equal(eager.counts[:, :n], graphed.counts[:, :n]) and
+                             torch.equal(lat_e.owned(), lat_g.owned())))
+        q.put((rank, same, graphed.step_index, len(step.graphs[1])))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,halo', [(2, 100), (3, 7)])
+def test_banded_step_graph_replay_equals_eager(world, halo):
+    """Colony.capture_banded: each rank's step replayed as [kinetics + gather +
+    uniform probe] and one graph per halo block, with the halo exchanges and
+    the uniform all-reduce issued eagerly between them, equals the eager
+    banded step bit for bit on every rank, every step (a band-deep halo: 5
+    blocks of 20 substeps; halo 7: 15 blocks)."""
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    halo = min(halo, NX // world)
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, halo, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    parts = sorted([q.get(timeout=150) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same, steps, blocks in parts:
+        assert all(same), (rank, same)
+        assert steps == GSTEPS + 1
+        assert blocks == -(-100 // halo)
+
+
+def _c2_graph_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from lens_amd import configs
+        from lens_amd.colony import Colony
+        from lens_amd.rate_law_compiler import compile_rate_laws
+        dev = torch.device('cuda', 0)
+        torch.cuda.set_device(dev)
+        cfg = configs.glc_lct_config()
+        t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+        n_all = 3000
+        params, conc = configs.heterogeneous_colony(t, cfg, n_all)
+        lo, hi = n_all * rank // world, n_all * (rank + 1) // world
+        cols = []
+        for _ in range(2):
+            c = Colony(cfg, hi - lo, device=dev, integrator='dopri5', table=t, specialize=True)
+            c.set_agents(params=params[:, lo:hi], conc=conc[:, lo:hi])
+            c.step(1.0)
+            cols.append(c)
+        replay = cols[1].capture(1.0, 5)        # an agent shard: no per-step collective
+        for _ in range(2):
+            for _ in range(5):
+                cols[0].step(1.0)
+            replay()
+        torch.cuda.synchronize()
+        q.put((rank, bool(torch.equal(cols[0].conc, cols[1].conc) and torch.equal(cols[0].h_state, cols[1].h_state))))
+    finally:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def test_sharded_c2_graph_replay_equals_eager():
+    """C2 on 2 ranks (agents sharded by index, no per-step collective): each
+    rank's colony replays its steps from a HIP graph, bit-identical to eager."""
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c2_graph_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    parts = [q.get(timeout=150) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok in parts)
