@@ -562,27 +562,34 @@ def main():
         attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
     split = None
     if use_graph and not banded:
-        # kernel times of the replayed step: a graph of the same steps with HIP events
-        # recorded inside it (external event nodes), replayed after the timed region
-        try:
-            replay_t = col.capture(1.0, per_graph, timing=True)
-            replay_t()
-            replay_t()
+        # kernel times of the replayed step's parts: HIP graphs of per_graph kinetics
+        # launches / per_graph diffusion calls, each timed with HIP events around
+        # its replay (after the timed region; torch refuses graph-internal events
+        # on ROCm), so no Python launch overhead enters the split
+        def graph_ms(fn):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(per_graph):
+                    fn()
+            g.replay()
+            e0, e1 = ev(), ev()
             barrier()
-            marks = replay_t.timing
-            split = {'step_kernels_ms': float(np.mean([m['step'][0].elapsed_time(m['step'][1]) for m in marks])),
-                     'kin_ms': float(np.mean([m['kin'][0].elapsed_time(m['kin'][1]) for m in marks])),
-                     'diff_ms': float(np.mean([m['diff'][0].elapsed_time(m['diff'][1]) for m in marks]))
-                     if lat is not None else None,
-                     'from': 'HIP events inside a captured graph of %d steps, replayed after the timed region'
-                             % per_graph}
+            e0.record()
+            g.replay()
+            e1.record()
+            barrier()
+            return e0.elapsed_time(e1) / per_graph
+        try:
+            split = {'kin_ms': graph_ms(lambda: col.kinetics(1.0)),
+                     'diff_ms': graph_ms(lambda: lat.diffuse(1.0)) if lat is not None else None,
+                     'from': 'HIP-graph replays of %d kinetics launches / %d diffusion calls (uniform probe + '
+                             'fused passes), timed with HIP events, after the timed region' % (per_graph, per_graph)}
         except Exception as exc:            # pragma: no cover - reported, then the eager fallback
             split = {'error': repr(exc)}
     if split is not None and 'kin_ms' in split:
         kin_ms, diff_ms = split['kin_ms'], split['diff_ms']
         if graph_info is not None:
             graph_info['kernel_split_from'] = split['from']
-            graph_info['step_kernels_ms'] = split['step_kernels_ms']
     elif lat is None and use_graph:     # the replayed step is the kinetics launch
         kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
         diff_ms = None

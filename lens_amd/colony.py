@@ -410,7 +410,7 @@ class Colony:
                 lat.exchange_atomic(self.bin_lin, self.n, self.counts, self.map_exch_count,
                                     self.map_exch_field)
 
-    def capture(self, dt: float = 1.0, steps: int = 1, timing: bool = False):
+    def capture(self, dt: float = 1.0, steps: int = 1):
         """Capture ``steps`` timesteps into one HIP graph (torch.cuda.CUDAGraph)
         and return a function that replays them.
 
@@ -426,13 +426,7 @@ class Colony:
         so the colony state is unchanged until the first replay. The graph
         holds the buffers and the agent count of capture time: set_agents()
         values may change between replays (they are copied in place), but a
-        re-binning of moved agents invalidates it (replay raises).
-
-        ``timing=True`` also records HIP events inside the graph (external
-        event-record nodes, :class:`lens_amd.graph_events.GraphEvent`) around every captured step, its kinetics launch
-        and its diffusion passes: ``replay.timing`` is the list of per-step
-        ``{'step', 'kin', 'diff'}`` event pairs, holding the last replay's
-        kernel times."""
+        re-binning of moved agents invalidates it (replay raises)."""
         lat = self.lattice
         if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
                 (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
@@ -444,19 +438,9 @@ class Colony:
         graph = torch.cuda.CUDAGraph()
         t0, s0 = self.time, self.step_index
         layout, n = self._layout, self.n
-        marks = None
-        if timing:
-            from lens_amd.graph_events import GraphEvent     # torch refuses external events on ROCm
-            ev = GraphEvent
-            marks = [{'step': (ev(), ev()), 'kin': (ev(), ev()),
-                      'diff': (ev(), ev()) if lat is not None else None} for _ in range(steps)]
         with torch.cuda.graph(graph):
-            for k in range(steps):
-                if marks:
-                    marks[k]['step'][0].record()
-                self.step(dt, timing=marks[k] if marks else None)
-                if marks:
-                    marks[k]['step'][1].record()
+            for _ in range(steps):
+                self.step(dt)
         self.time, self.step_index = t0, s0      # capture ran nothing
 
         def replay():
@@ -469,7 +453,6 @@ class Colony:
             self.step_index += steps
 
         replay.graph = graph      # keep the graph (and its memory pool) alive with the replayer
-        replay.timing = marks
         return replay
 
     def capture_banded(self, dt: float = 1.0, halo_exchange=None, allreduce=None):
