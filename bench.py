@@ -196,6 +196,48 @@ def time_stencil_pass(lat, depth, reps=20):
     return e0.elapsed_time(e1) / reps
 
 
+def segment_split(col, steps, barrier):
+    """Kernel time of each part of the replayed step, measured in the step's own
+    sequence: the step is captured as three HIP graphs -- [kinetics], [gather +
+    uniform probe + fused passes], [exchange scatter] -- and `steps` steps are
+    replayed with HIP events recorded between the graph replays (torch refuses
+    events inside a graph on ROCm).  The GPU runs the three replays back to back
+    (the host issues them far faster than they run), so each event pair brackets
+    that part's kernels, with the caches as the previous part left them.  Run
+    after the timed region; advances the colony by `steps` steps."""
+    lat = col.lattice
+    segs = [lambda: col.kinetics(1.0)]
+    if lat is not None:
+        def diffuse():
+            col.gather_external()
+            lat.diffuse(1.0)
+        segs += [diffuse, col._step_exchange]
+    graphs = []
+    for fn in segs:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        graphs.append(g)
+    for g in graphs:                      # upload
+        g.replay()
+    barrier()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(graphs) + 1)] for _ in range(steps)]
+    for k in range(steps):
+        ev[k][0].record()
+        for i, g in enumerate(graphs):
+            g.replay()
+            ev[k][i + 1].record()
+    barrier()
+    part = lambda i: float(np.mean([ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(steps)]))
+    out = {'kin_ms': part(0), 'diff_ms': part(1) if lat is not None else None,
+           'exchange_ms': part(2) if lat is not None else None,
+           'from': 'the step replayed as 3 HIP graphs (kinetics | gather + diffusion | exchange) with HIP events '
+                   'between the replays, %d steps after the timed region' % steps}
+    col.time += steps
+    col.step_index += steps
+    return out
+
+
 def time_copy_floor(lat, reps=20):
     """Average duration of a plain device copy of the planes a pass streams
     (fields -> work0: one 8-B read + one 8-B write per cell, the algorithmic
@@ -562,34 +604,15 @@ def main():
         attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
     split = None
     if use_graph and not banded:
-        # kernel times of the replayed step's parts: HIP graphs of per_graph kinetics
-        # launches / per_graph diffusion calls, each timed with HIP events around
-        # its replay (after the timed region; torch refuses graph-internal events
-        # on ROCm), so no Python launch overhead enters the split
-        def graph_ms(fn):
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                for _ in range(per_graph):
-                    fn()
-            g.replay()
-            e0, e1 = ev(), ev()
-            barrier()
-            e0.record()
-            g.replay()
-            e1.record()
-            barrier()
-            return e0.elapsed_time(e1) / per_graph
         try:
-            split = {'kin_ms': graph_ms(lambda: col.kinetics(1.0)),
-                     'diff_ms': graph_ms(lambda: lat.diffuse(1.0)) if lat is not None else None,
-                     'from': 'HIP-graph replays of %d kinetics launches / %d diffusion calls (uniform probe + '
-                             'fused passes), timed with HIP events, after the timed region' % (per_graph, per_graph)}
+            split = segment_split(col, per_graph, barrier)
         except Exception as exc:            # pragma: no cover - reported, then the eager fallback
             split = {'error': repr(exc)}
     if split is not None and 'kin_ms' in split:
         kin_ms, diff_ms = split['kin_ms'], split['diff_ms']
         if graph_info is not None:
             graph_info['kernel_split_from'] = split['from']
+            graph_info['exchange_ms'] = split.get('exchange_ms')
     elif lat is None and use_graph:     # the replayed step is the kinetics launch
         kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
         diff_ms = None
@@ -646,15 +669,16 @@ def main():
             launch_ms = stencil_pass_ms
             bytes_per_launch = 16.0 * cells          # algorithmic: read + write each cell once
             achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
-            traffic = valu = None
-            pmc = os.path.join(REPO, 'profiles', 'pmc_stencil.json')
-            if os.path.exists(pmc) and world == 1:
+            traffic = valu = traffic_from = None
+            import glob
+            for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_stencil*.json'))) if world == 1 else []:
                 with open(pmc) as f:
                     rec = json.load(f)
-                # the committed PMC pass must describe this exact launch geometry
+                # the committed PMC pass must describe this exact launch geometry and mode
                 if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant'),
                         rec.get('mode', 'exact')) == (depth, args.stencil_rows, cells, args.stencil_kernel,
                                                       args.stencil_mode):
+                    traffic_from = os.path.relpath(pmc, REPO)
                     traffic = rec.get('hbm_bytes_per_launch')
                     if rec.get('valu_insts_per_launch') and rec.get('clock_ghz'):
                         # the pass against the VALU-issue bound: one wave64 VALU instruction
@@ -667,7 +691,7 @@ def main():
             kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode)
             roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
-                        'traffic': traffic, 'bytes_per_launch': bytes_per_launch,
+                        'traffic': traffic, 'traffic_from': traffic_from, 'bytes_per_launch': bytes_per_launch,
                         'avg_launch_ms': launch_ms, 'substeps_per_launch': depth,
                         'effective_stencil_gbps': bytes_per_launch * depth / (launch_ms * 1e-3) / 1e9,
                         'fp64_tflops': 6.0 * cells * depth / (launch_ms * 1e-3) / 1e12,
