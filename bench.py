@@ -59,6 +59,7 @@ WORKLOADS = {
 KREMLING_RHS_FLOPS = 71
 N_SIMDS = 256 * 4          # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 KREMLING_NY = 15
+SPLIT_STEPS = 6            # eager steps timed for the kinetics / diffusion split (the first is dropped)
 
 
 def stencil_kernel_name(variant, depth, mode='exact'):
@@ -194,48 +195,6 @@ def time_stencil_pass(lat, depth, reps=20):
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
-
-
-def segment_split(col, steps, barrier):
-    """Kernel time of each part of the replayed step, measured in the step's own
-    sequence: the step is captured as three HIP graphs -- [kinetics], [gather +
-    uniform probe + fused passes], [exchange scatter] -- and `steps` steps are
-    replayed with HIP events recorded between the graph replays (torch refuses
-    events inside a graph on ROCm).  The GPU runs the three replays back to back
-    (the host issues them far faster than they run), so each event pair brackets
-    that part's kernels, with the caches as the previous part left them.  Run
-    after the timed region; advances the colony by `steps` steps."""
-    lat = col.lattice
-    segs = [lambda: col.kinetics(1.0)]
-    if lat is not None:
-        def diffuse():
-            col.gather_external()
-            lat.diffuse(1.0)
-        segs += [diffuse, col._step_exchange]
-    graphs = []
-    for fn in segs:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            fn()
-        graphs.append(g)
-    for g in graphs:                      # upload
-        g.replay()
-    barrier()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(graphs) + 1)] for _ in range(steps)]
-    for k in range(steps):
-        ev[k][0].record()
-        for i, g in enumerate(graphs):
-            g.replay()
-            ev[k][i + 1].record()
-    barrier()
-    part = lambda i: float(np.mean([ev[k][i].elapsed_time(ev[k][i + 1]) for k in range(steps)]))
-    out = {'kin_ms': part(0), 'diff_ms': part(1) if lat is not None else None,
-           'exchange_ms': part(2) if lat is not None else None,
-           'from': 'the step replayed as 3 HIP graphs (kinetics | gather + diffusion | exchange) with HIP events '
-                   'between the replays, %d steps after the timed region' % steps}
-    col.time += steps
-    col.step_index += steps
-    return out
 
 
 def time_copy_floor(lat, reps=20):
@@ -469,7 +428,7 @@ def main():
     mk = lambda: ({'kin': (ev(), ev()), 'diff': (ev(), ev())} if lat is not None else {'kin': (ev(), ev())})
     # Per-step bookkeeping inside the timed region is kept to what cannot be had
     # afterwards.  Lattice steps record no HIP events (the kinetics / diffusion
-    # split comes from one eager step after the timed region).  A non-dividing
+    # split comes from eager steps after the timed region).  A non-dividing
     # colony integrates the same agents every step, so its DP45 attempts are read
     # from the last step's per-agent counts (a per-step torch reduction or device
     # copy of the counts is a launch of its own in every step).  Eager vs graph
@@ -602,34 +561,30 @@ def main():
         attempts_from = 'colony sum after every kinetics launch'
     else:                             # same agents every step (no division): last step x steps
         attempts = float(col.nsteps[:col.n].sum().item()) * args.steps
-    split = None
-    if use_graph and not banded:
-        try:
-            split = segment_split(col, per_graph, barrier)
-        except Exception as exc:            # pragma: no cover - reported, then the eager fallback
-            split = {'error': repr(exc)}
-    if split is not None and 'kin_ms' in split:
-        kin_ms, diff_ms = split['kin_ms'], split['diff_ms']
-        if graph_info is not None:
-            graph_info['kernel_split_from'] = split['from']
-            graph_info['exchange_ms'] = split.get('exchange_ms')
-    elif lat is None and use_graph:     # the replayed step is the kinetics launch
+    if lat is None and use_graph:     # the replayed step is the kinetics launch
         kin_ms = e_all[0].elapsed_time(e_all[1]) / args.steps
         diff_ms = None
     elif lat is None:
         kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
         diff_ms = None
     else:
-        # the kinetics / diffusion split of the report: one eager step after the timed region
-        t_one = mk()
-        one_step(t_one)
+        # The kinetics / diffusion split: eager steps after the timed region with
+        # HIP events around the kinetics launch and the diffusion passes.  A
+        # lattice step is ~10x longer on the GPU than its issue from Python, so
+        # from the second step on the host runs ahead and the events bracket
+        # kernel time only (the first step still waits for its issue: dropped).
+        # (Segment graphs timed between replays add each graph launch's GPU-side
+        # gap, ~10 us, and torch refuses events inside a graph on ROCm.)
+        marks = [mk() for _ in range(SPLIT_STEPS)]
         barrier()
-        kin_ms = t_one['kin'][0].elapsed_time(t_one['kin'][1])
-        diff_ms = t_one['diff'][0].elapsed_time(t_one['diff'][1])
+        for t_k in marks:
+            one_step(t_k)
+        barrier()
+        kin_ms = float(np.median([t['kin'][0].elapsed_time(t['kin'][1]) for t in marks[1:]]))
+        diff_ms = float(np.median([t['diff'][0].elapsed_time(t['diff'][1]) for t in marks[1:]]))
         if graph_info is not None:
-            graph_info['kernel_split_from'] = 'one eager step after the timed region'
-            if split is not None:
-                graph_info['graph_timing_error'] = split.get('error')
+            graph_info['kernel_split_from'] = ('median of %d eager steps after the timed region (HIP events; the '
+                                               'host issues ahead of the GPU after the first)' % (SPLIT_STEPS - 1))
     if dist is not None:
         if args.dist_backend == 'gloo':
             el, n_agents = el.cpu(), n_agents.cpu()

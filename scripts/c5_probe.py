@@ -1,6 +1,6 @@
 """Time the agent-per-wavefront DP45 on the C5 network (50 species, 40 reactions):
-the table walk (variant 1) against the specialised kernel (variant 3) compiled
-for 2 and 3 waves per SIMD.
+the table walk (variant 1) against the specialised kernel (variant 3), with and
+without branch-free LDS publishes (KineticsEngine.WAVE_PAD_WRITES).
 
     python scripts/c5_probe.py [n_agents]
 """
@@ -18,10 +18,12 @@ print('ny', t.n_dyn + t.n_reactions, 'rate laws', t.n_rate_laws, 'F_rhs', t.flop
 params, conc = configs.heterogeneous_colony(t, cfg, n, sigma=0.2)
 P = torch.from_numpy(params).to(dev)
 m2c = torch.full((n,), 7e5, dtype=torch.float64, device=dev)
-for label, variant, wpe in (('generic', 1, None), ('spec-3w', 3, 3)):
+cases = [('generic', 1, None, 0), ('spec-2w', 3, 2, 0), ('spec-2w-pad', 3, 2, 1)]
+for label, variant, wpe, pad in cases + cases[1:]:      # A/B/A/B in one process
     eng = KineticsEngine(t, dev)
     if wpe:
         eng.WAVE_WAVES_PER_SIMD = wpe
+        eng.WAVE_PAD_WRITES = pad
         eng.specialize()
     C = torch.from_numpy(conc).to(dev)
     h = torch.zeros(n, dtype=torch.float64, device=dev)

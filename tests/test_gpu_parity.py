@@ -293,12 +293,14 @@ def _two_enzyme_network(n=96, seed=20261016):
     return cfg, t, params, conc
 
 
+@pytest.mark.parametrize('pad', [0, 1])
 @pytest.mark.parametrize('net', ['c5', 'two_enzyme', 'wide'])
-def test_dopri5_wave_spec_equals_generic_wave(dev, net):
+def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad):
     """The specialised wavefront kernel (variant 3) against the table walk
     (variant 1): the padded identities are exact and everything else is the
     same arithmetic in the same order, so states, fluxes, counts, step counts
-    and carried step sizes agree bit for bit."""
+    and carried step sizes agree bit for bit -- with the branch-free LDS
+    publishes (pad = 1, padding lanes write a scratch slot) too."""
     from lens_amd import codegen
     if net == 'c5':
         cfg, t, params, conc = _big_network(n=300)
@@ -311,6 +313,7 @@ def test_dopri5_wave_spec_equals_generic_wave(dev, net):
     n = conc.shape[1]
     m2c = torch.full((n,), mmol_to_counts(), dtype=torch.float64, device=dev)
     eng = _engine(t, dev)
+    eng.WAVE_PAD_WRITES = pad
     out = []
     for variant in (1, 3):
         if variant == 3:
