@@ -3,7 +3,7 @@
 substeps, each block preceded by a local stand-in for the halo exchange (the
 same 4 row-copies per field the real exchange does; no RCCL).  Prints ms per step.
 
-    python scripts/rank_emulate.py N halo rows [variant depth]
+    python scripts/rank_emulate.py N halo rows [variant depth [mode]]     (mode: exact | fma)
 """
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -14,6 +14,9 @@ from lens_amd.distributed import row_bands
 world, halo, rows = (int(x) for x in sys.argv[1:4])
 variant = int(sys.argv[4]) if len(sys.argv) > 4 else 3
 depth = int(sys.argv[5]) if len(sys.argv) > 5 else 9
+mode = sys.argv[6] if len(sys.argv) > 6 else 'exact'
+from lens_amd.lattice import stencil_mode
+stencil_mode(mode)
 dev = torch.device('cuda', 0)
 nx = 4096
 band = row_bands(nx, world)[1 if world > 2 else 0]
@@ -41,5 +44,5 @@ for _ in range(10):
     lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
 torch.cuda.synchronize()
 ms = (time.perf_counter() - t0) / 10 * 1e3
-print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d: %.3f ms/step (ideal %.3f = 1/N of the whole)' % (
-    world, band, halo, rows, variant, depth, ms, 1.95 / world))
+print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step (ideal %.3f = 1/N of the whole)' % (
+    world, band, halo, rows, variant, depth, mode, ms, 1.95 / world))
