@@ -601,6 +601,10 @@ def main():
         kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec', 3: 'vk_dopri5_wspec'}[variant]
         integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / agent_steps,
+                 # integrator steps (accepted + rejected) and RHS evaluations
+                 # per second over the timed region (rank 0; DP45 with FSAL: 6 new RHS per attempt)
+                 'dp45_attempts_per_s': attempts / elapsed if elapsed else None,
+                 'rhs_evals_per_s': 6.0 * attempts / elapsed if elapsed else None,
                  'dp45_attempts_per_agent_step_by_step': per_step, 'attempts_from': attempts_from,
                  'flops_per_attempt': col.engine.dopri5_flops_per_attempt(),
                  'achieved_tflops': integ_flops / (kin_ms * 1e-3) / 1e12 if kin_ms else None,
