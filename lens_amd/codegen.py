@@ -157,7 +157,7 @@ def _table(name: str, ctype: str, rows) -> str:
     return '__device__ const %s %s%s = %s;' % (ctype, name, ''.join('[%d]' % d for d in dims), rec(rows))
 
 
-def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0) -> str:
+def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int = 0) -> str:
     """Complete HIP source of the specialised agent-per-wavefront kernel ``vk_dopri5_wspec``."""
     sh = wave_shape(t)
     W = WAVE_LANES
@@ -211,7 +211,7 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0) -> str:
         ('NS', ns), ('ND', nd), ('NR', nr), ('NL', nl), ('NY', ny), ('LR', LR), ('SN', SN), ('MN', MN),
         ('SD', SD), ('MD', MD), ('NSLOT', NSLOT), ('UM', UM), ('RX_IDENTITY', sh['RX_IDENTITY']),
         ('RXR', RXR), ('RXM', RXM), ('TILE', ns + 1 + nr + 1 + nl + 1 + (W if pad_writes else 0)), ('WPE', wpe),
-        ('PAD_WRITES', int(pad_writes))])
+        ('PAD_WRITES', int(pad_writes)), ('LDS_OPS', int(lds_ops))])
     umk = [max([int(t.upd_ptr[i + 1] - t.upd_ptr[i]) for i in range(k * W, min(nd, (k + 1) * W))] or [0])
            for k in range(NSLOT)]
     defs += '\n__device__ constexpr int UMK[NSLOT] = {%s};' % ', '.join(str(u) for u in umk)

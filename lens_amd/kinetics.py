@@ -53,7 +53,7 @@ class KineticsEngine:
             # instead, while its padded per-lane operands fit the register file
             if wave_registers(self.table) > self.WAVE_REGISTER_LIMIT:
                 return self
-            src = wave_source(self.table, self.WAVE_WAVES_PER_SIMD, self.WAVE_PAD_WRITES)
+            src = wave_source(self.table, self.WAVE_WAVES_PER_SIMD, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS)
         else:
             src = dopri5_source(self.table)
         with torch.cuda.device(self.device):
@@ -63,7 +63,9 @@ class KineticsEngine:
 
     LANE_LIMIT = 32   # integrated components an agent-per-lane kernel holds in VGPRs
     WAVE_REGISTER_LIMIT = 270   # codegen.wave_registers estimate beyond which variant 1 stays (spills)
-    WAVE_PAD_WRITES = 0         # 1: branch-free LDS publishes (padding lanes write a scratch slot)
+    WAVE_PAD_WRITES = 1         # 1: branch-free LDS publishes (padding lanes write a scratch slot;
+                                # C5 113.5 -> 111.9 ms, profiles/r03/r03e_c5_probe.log)
+    WAVE_LDS_OPS = 0            # 1: denominator 1/Km and stoichiometry read from LDS tables (fewer VGPRs)
     WAVE_WAVES_PER_SIMD = 2     # occupancy the specialised wavefront kernel is compiled for: with its gathers
                                 # batched it needs 216 VGPRs (C5: 2 waves 120.5 ms; 3 waves spill, 224 ms)
 

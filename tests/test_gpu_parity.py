@@ -293,14 +293,15 @@ def _two_enzyme_network(n=96, seed=20261016):
     return cfg, t, params, conc
 
 
-@pytest.mark.parametrize('pad', [0, 1])
+@pytest.mark.parametrize('pad,lds', [(0, 0), (1, 0), (1, 1)])
 @pytest.mark.parametrize('net', ['c5', 'two_enzyme', 'wide'])
-def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad):
+def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad, lds):
     """The specialised wavefront kernel (variant 3) against the table walk
     (variant 1): the padded identities are exact and everything else is the
     same arithmetic in the same order, so states, fluxes, counts, step counts
     and carried step sizes agree bit for bit -- with the branch-free LDS
-    publishes (pad = 1, padding lanes write a scratch slot) too."""
+    publishes (pad = 1, padding lanes write a scratch slot) and the operand
+    tables in LDS (lds = 1) too."""
     from lens_amd import codegen
     if net == 'c5':
         cfg, t, params, conc = _big_network(n=300)
@@ -314,6 +315,7 @@ def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad):
     m2c = torch.full((n,), mmol_to_counts(), dtype=torch.float64, device=dev)
     eng = _engine(t, dev)
     eng.WAVE_PAD_WRITES = pad
+    eng.WAVE_LDS_OPS = lds
     out = []
     for variant in (1, 3):
         if variant == 3:
