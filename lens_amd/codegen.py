@@ -162,6 +162,8 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int
     sh = wave_shape(t)
     W = WAVE_LANES
     ns, nr, nl, nd = t.n_species, t.n_reactions, t.n_rate_laws, t.n_dyn
+    if lds_ops >= 2 and ns + 1 > 32767:
+        raise ValueError('lds_ops=2 keeps species indices in 16 bits')
     ny = nd + nr
     LR, SN, MN, SD, MD = sh['LR'], sh['SN'], sh['MN'], sh['SD'], sh['MD']
     PAD_SP = ns   # cl[NS] == 1.0

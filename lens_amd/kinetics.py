@@ -65,7 +65,8 @@ class KineticsEngine:
     WAVE_REGISTER_LIMIT = 270   # codegen.wave_registers estimate beyond which variant 1 stays (spills)
     WAVE_PAD_WRITES = 1         # 1: branch-free LDS publishes (padding lanes write a scratch slot;
                                 # C5 113.5 -> 111.9 ms, profiles/r03/r03e_c5_probe.log)
-    WAVE_LDS_OPS = 0            # 1: denominator 1/Km and stoichiometry read from LDS tables (fewer VGPRs)
+    WAVE_LDS_OPS = 0            # 1: denominator 1/Km and stoichiometry read from LDS tables (fewer VGPRs);
+                                # 2: also the denominator member indices
     WAVE_WAVES_PER_SIMD = 2     # occupancy the specialised wavefront kernel is compiled for: with its gathers
                                 # batched it needs 216 VGPRs (C5: 2 waves 120.5 ms; 3 waves spill, 224 ms)
 

@@ -19,7 +19,8 @@ print('ny', t.n_dyn + t.n_reactions, 'rate laws', t.n_rate_laws, 'F_rhs', t.flop
 params, conc = configs.heterogeneous_colony(t, cfg, n, sigma=0.2)
 P = torch.from_numpy(params).to(dev)
 m2c = torch.full((n,), 7e5, dtype=torch.float64, device=dev)
-cases = [('generic', 1, None, 1, 0), ('spec-2w', 3, 2, 1, 0), ('spec-2w-lds', 3, 2, 1, 1), ('spec-3w-lds', 3, 3, 1, 1)]
+cases = [('generic', 1, None, 1, 0), ('spec-2w', 3, 2, 1, 0), ('spec-2w-lds1', 3, 2, 1, 1), ('spec-3w-lds1', 3, 3, 1, 1),
+         ('spec-2w-lds2', 3, 2, 1, 2), ('spec-3w-lds2', 3, 3, 1, 2)]
 for label, variant, wpe, pad, lds in cases + cases[1:]:      # A/B/A/B in one process
     eng = KineticsEngine(t, dev)
     if wpe:

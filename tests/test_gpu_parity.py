@@ -293,7 +293,7 @@ def _two_enzyme_network(n=96, seed=20261016):
     return cfg, t, params, conc
 
 
-@pytest.mark.parametrize('pad,lds', [(0, 0), (1, 0), (1, 1)])
+@pytest.mark.parametrize('pad,lds', [(0, 0), (1, 0), (1, 1), (1, 2)])
 @pytest.mark.parametrize('net', ['c5', 'two_enzyme', 'wide'])
 def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad, lds):
     """The specialised wavefront kernel (variant 3) against the table walk
