@@ -60,3 +60,15 @@ def test_generated_rhs_matches_reference_fluxes(golden_fluxes):
             got = dy[t.n_dyn:]
             ref = np.array([expect[r] for r in t.reaction_ids])
             np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-300)
+
+
+@pytest.mark.parametrize('wpe,pad,lds', [(2, 0, 0), (2, 1, 0), (3, 1, 1), (3, 1, 2)])
+def test_wave_source_compiles_for_gfx950(wpe, pad, lds, tmp_path):
+    """The agent-per-wavefront template (C5 network) in every option
+    combination the engine can select: occupancy, branch-free publishes, LDS
+    operand tables (levels 1 and 2).  hiprtc compiles the same text at run
+    time on the GPU; this catches template errors on the CPU."""
+    from lens_amd.codegen import wave_source
+    cfg = configs.synthetic_network()
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    _hipcc_compile('#include <hip/hip_runtime.h>\n' + wave_source(t, wpe, pad, lds), tmp_path)
