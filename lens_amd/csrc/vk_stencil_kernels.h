@@ -181,6 +181,7 @@ __device__ __forceinline__ void wl_store(double *o, double2 v) {
 struct WtLane {
     int cA;              // this lane's first column (cB = cA + 1)
     int ny;
+    uint32_t voff;       // VK_WL_BUF_STORE: byte offset of column A in its row, out of range (store dropped) if not wA
     bool wA, wB;         // writes its column A / B
     bool lA, rA, lB, rB; // reflect flags (EDGE tiles only)
 };
@@ -204,9 +205,24 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
 // the iteration phase U (period 3): up = S[U], centre = S[U+1], fresh = S[U+2].
 // ---------------------------------------------------------------------------
 
+// VK_WL_RING (variant 12/13): stage 0 reads its three rows straight from the
+// prefetch ring, which then holds PD + 3 rows (up, centre, fresh and PD in
+// flight), and the loop is unrolled by that ring length.  Without it the ring
+// (PD slots) and the stage-0 window (3 slots) rotate with different periods, so
+// the register allocator closes each unrolled group with copies of the
+// in-flight rows -- and a vmcnt(0) before them, which drains every load (and
+// streaming store) once per group of PD rows.
+#ifdef VK_WL_RING
+constexpr int wl_ring(int PD) { return PD + 3; }
+constexpr bool WL_RING = true;
+#else
+constexpr int wl_ring(int PD) { return PD; }
+constexpr bool WL_RING = false;
+#endif
+
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
 template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool STEADY, int U>
-__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
+__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[wl_ring(PD)], double2 (&gp)[3],
                                         const double *__restrict__ s, double *d,
                                         const double *g, const WtLane &L, int i, int c0, int c1,
                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
@@ -216,8 +232,21 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     double2(&CN)[K] = R == 0 ? S1 : (R == 1 ? S2 : S0);
     double2(&FR)[K] = R == 0 ? S2 : (R == 1 ? S0 : S1);
     const int64_t ny = L.ny;
-    FR[0] = pf[U];                                                                          // row i
-    pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L);     // row i+PD
+#ifdef VK_WL_BUF_STORE
+    // keep each iteration's load, stages and store in program order: with the
+    // stores branch-free, a steady group of PD iterations is one basic block, and
+    // the scheduler would otherwise cluster its PD loads at the end of the block
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+    constexpr int NR = wl_ring(PD);
+    if constexpr (WL_RING) {
+        // row j lives in slot (j - i0) mod NR; U = (i - i0) mod NR.  Row i+PD goes
+        // to the slot of row i-3, whose last use (as stage 0's up row) was iteration i-1
+        pf[(U + PD) % NR] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L);
+    } else {
+        FR[0] = pf[U];                                                                      // row i
+        pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L); // row i+PD
+    }
     const int r_out = i - K;
     const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
     double2 base = make_double2(0.0, 0.0);
@@ -230,9 +259,10 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
         // stage q is useful for rows [c0-(K-1-q), c1+(K-1-q)), i.e. i in [c0-K+2+2q, c1+K)
         if (!STEADY && (i < c0 - K + 2 + 2 * q || i >= c1 + K)) continue;
         const int r = i - 1 - q;
-        const double2 cen = CN[q];
-        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
-        const double2 dn = (EDGE && r == bot_reflect) ? cen : FR[q];
+        const bool ring0 = WL_RING && q == 0;
+        const double2 cen = ring0 ? pf[(U + NR - 1) % NR] : CN[q];
+        const double2 up = (EDGE && r == top_reflect) ? cen : (ring0 ? pf[(U + NR - 2) % NR] : UP[q]);
+        const double2 dn = (EDGE && r == bot_reflect) ? cen : (ring0 ? pf[U % NR] : FR[q]);
         double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
         double rightA = cen.y, leftB = cen.x;
         if (EDGE) {
@@ -259,7 +289,21 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
             if (FINAL && !FAST) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
             double *o = d + (int64_t)r_out * ny + L.cA;
             if (!EDGE) {
+#ifdef VK_WL_BUF_STORE
+                // Branch-free store: lanes that do not write carry an out-of-range
+                // offset and the buffer unit drops their store.  With no exec branch
+                // around the store, the compiler's vmcnt bookkeeping counts every
+                // iteration's store, so a row load is awaited only PD rows after its
+                // issue (a masked store made it wait as if no store were in flight:
+                // about PD/2 rows of lookahead).  aux 2 = nt (streaming store).
+                (void)o;
+                typedef int i4v __attribute__((ext_vector_type(4)));
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    (void *)(d + (int64_t)r_out * ny), 0, (int)(ny * 8), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v), rs, (int)L.voff, 0, 2);
+#else
                 if (L.wA) wl_store(o, v);
+#endif
             } else {
                 if (L.wA) o[0] = v.x;
                 if (L.wB) o[1] = v.y;
@@ -270,7 +314,7 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
 
 template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
-                                         double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *d,
+                                         double2 (&pf)[wl_ring(PD)], double2 (&gp)[3], const double *__restrict__ s, double *d,
                                          const double *g, const WtLane &L, int i, int c0, int c1,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
                                          double c4) {
@@ -283,7 +327,7 @@ __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], dou
 
 template <int K, int PD, bool EDGE, bool FINAL, bool FAST, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
-                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
+                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[wl_ring(PD)], double2 (&gp)[3],
                                                 const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
@@ -291,11 +335,18 @@ __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...
     const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
     const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
 #define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4
+    constexpr int NU = wl_ring(PD);                  // iterations per unrolled group
     int i = i0;
-    for (; i + PD <= i1 && i < s_lo; i += PD) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);   // fill
-    for (; i + PD - 1 <= s_hi; i += PD) wl_group<K, PD, EDGE, FINAL, FAST, true, Us...>(WL_ARGS);          // steady
-    for (; i + PD <= i1; i += PD) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);               // drain
-    // tail: fewer than PD iterations, phases 0.. in order
+    for (; i + NU <= i1 && i < s_lo; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);   // fill
+#ifdef VK_WL_BUF_STORE
+    // enter the steady loop with no memory operation in flight, so that the
+    // compiler's wait counts at its header come from the loop's own (branch-free)
+    // iterations and not from the fill phase's conditional stores
+    if (!EDGE) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+#endif
+    for (; i + NU - 1 <= s_hi; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, true, Us...>(WL_ARGS);          // steady
+    for (; i + NU <= i1; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);               // drain
+    // tail: fewer than NU iterations, phases 0.. in order
     ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, FAST, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1,
                                                               in_lo, in_hi, top_reflect, bot_reflect, coef, c4)
                   : void()), ...);
@@ -307,14 +358,18 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef, double c4) {
-    double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
+    constexpr int NR = wl_ring(PD);
+    double2 S0[K], S1[K], S2[K], pf[NR], gp[3];
 #pragma unroll
     for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
     const int64_t ny = L.ny;
     const int i0 = c0 - K + 2;
     // stage 0's window before the first iteration: up = row i0-2, centre = row i0-1
-    S0[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 2, in_lo), in_hi - 1) * ny, L);
-    S1[0] = wt_load<EDGE>(s, (int64_t)min(max(i0 - 1, in_lo), in_hi - 1) * ny, L);
+    // (ring: slots NR-2 and NR-1)
+    double2 &w_up = WL_RING ? pf[NR - 2] : S0[0];
+    double2 &w_cn = WL_RING ? pf[NR - 1] : S1[0];
+    w_up = wt_load<EDGE>(s, (int64_t)min(max(i0 - 2, in_lo), in_hi - 1) * ny, L);
+    w_cn = wt_load<EDGE>(s, (int64_t)min(max(i0 - 1, in_lo), in_hi - 1) * ny, L);
 #pragma unroll
     for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
 #pragma unroll
@@ -322,7 +377,7 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
         gp[u] = FINAL && !FAST && (L.wA || L.wB)
                     ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
                     : make_double2(0.0, 0.0);
-    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L,
+    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST>(std::make_integer_sequence<int, NR>(), S0, S1, S2, pf, gp, s, d, g, L,
                                               c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
@@ -355,6 +410,7 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     const int cB = L.cA + 1;
     L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
     L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
+    L.voff = L.wA ? (uint32_t)L.cA * 8u : 0x80000000u;
     L.lA = L.cA == 0;
     L.rA = L.cA == ny - 1;
     L.lB = cB == 0;
@@ -385,8 +441,11 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     src, dst, f0, field_stride, ny, out_lo, out_hi, in_lo, in_hi, top_reflect, bot_reflect, rows_per_chunk,      \
         tiles_x, chunks_y, n_fields, coef, uniform
 
+#ifndef VK_WL_WAVES_ATTR
+#define VK_WL_WAVES_ATTR
+#endif
 template <int K, int PD, bool FINAL, bool FAST = false>
-__global__ __launch_bounds__(256) void k_diffuse_wl(VK_WL_PARAMS) {
+__global__ __launch_bounds__(256) VK_WL_WAVES_ATTR void k_diffuse_wl(VK_WL_PARAMS) {
     diffuse_wl_tile<K, PD, FINAL, FAST>(VK_WL_ARGS);
 }
 

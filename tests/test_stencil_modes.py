@@ -32,33 +32,33 @@ def dev():
 
 
 class _mode:
-    def __init__(self, mode, depth=None, rows=None):
-        self.mode, self.depth, self.rows = mode, depth, rows
+    def __init__(self, mode, depth=None, rows=None, variant=-1):
+        self.mode, self.depth, self.rows, self.variant = mode, depth, rows, variant
 
     def __enter__(self):
         from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
         self.prev = stencil_mode(self.mode)
         self.prev_d = stencil_depth(self.depth) if self.depth else None
-        self.prev_k = stencil_kernel(-1, self.rows) if self.rows else None
+        self.prev_k = stencil_kernel(self.variant, self.rows or 0)
 
     def __exit__(self, *exc):
         from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
         stencil_mode(self.prev)
         if self.prev_d:
             stencil_depth(self.prev_d)
-        if self.prev_k is not None:
-            stencil_kernel(-1, 0)
+        stencil_kernel(self.prev_k, 0)
 
 
 def _rel(got, ref):
     return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-300))
 
 
+@pytest.mark.parametrize('variant', [6, 12, 13])
 @pytest.mark.parametrize('depth', [7, 9, 11])
-def test_fma_mode_vs_scipy_goldens(dev, depth):
+def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
     from lens_amd.lattice import Lattice
     z = np.load(os.path.join(GOLDEN, 'stencil.npz'))
-    with _mode('fma', depth, 16):
+    with _mode('fma', depth, 16, variant):
         for shape in ('17x23', '64x64', '128x96'):
             f0 = z['f0_' + shape]
             nx, ny = f0.shape
@@ -71,14 +71,15 @@ def test_fma_mode_vs_scipy_goldens(dev, depth):
                 assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))
 
 
+@pytest.mark.parametrize('variant', [6, 12, 13])
 @pytest.mark.parametrize('depth,rows', [(9, 64), (7, 40), (11, 48), (9, 17)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
-def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape):
+def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape, variant):
     from lens_amd.lattice import Lattice
     rng = np.random.default_rng(9)
     nx, ny = shape
     f0 = rng.random((nx, ny)) + 0.5
-    with _mode('fma', depth, rows):
+    with _mode('fma', depth, rows, variant):
         lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
         lat.diffuse(1.0)
         got = lat.owned('a').cpu().numpy()
