@@ -157,14 +157,65 @@ def _table(name: str, ctype: str, rows) -> str:
     return '__device__ const %s %s%s = %s;' % (ctype, name, ''.join('[%d]' % d for d in dims), rec(rows))
 
 
-def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int = 0) -> str:
-    """Complete HIP source of the specialised agent-per-wavefront kernel ``vk_dopri5_wspec``."""
+def split_layout(t: RateLawTable):
+    """Lane layout of the split-denominator option (one round of <= 64 rate laws).
+
+    The P = min(nl, 64 - nl, 32) rate laws with the most denominator sets get
+    two lanes, l and l + 32: lane l takes the first ceil(n/2) sets and lane
+    l + 32 the rest.  Lane l + 32 hands its set terms (term - 1) to lane l over
+    v_permlane32_swap, and lane l adds them after its own in set order -- the
+    same sequential sum as one lane (kinetic_rate_laws.py:160-172), so the
+    result is bit-identical.  The other rate laws keep one lane each, in lanes
+    [P, 32) and [32 + P, 64).  Returns (lanes, dst, second, sets): per lane its
+    rate law (-1 idle), the rate law it writes (-1: the scratch slot), the
+    second-half flag and its (set_lo, set_hi) range; None if not applicable.
+    """
+    nl, W, H = t.n_rate_laws, WAVE_LANES, WAVE_LANES // 2
+    if nl == 0 or nl > W:
+        return None
+    nden = [int(t.rl_den_ptr[l + 1] - t.rl_den_ptr[l]) for l in range(nl)]
+    P = min(nl, W - nl, H)
+    order = sorted(range(nl), key=lambda l: (-nden[l], l))
+    heavy = sorted(order[:P])
+    single = sorted(order[P:])
+    lanes, dst, second = [-1] * W, [-1] * W, [0] * W
+    sets = [(0, 0)] * W
+    for i, l in enumerate(heavy):
+        a, b = i, i + H
+        lo, hi = int(t.rl_den_ptr[l]), int(t.rl_den_ptr[l + 1])
+        mid = lo + (hi - lo + 1) // 2
+        lanes[a] = lanes[b] = l
+        dst[a] = l
+        second[b] = 1
+        sets[a], sets[b] = (lo, mid), (mid, hi)
+    free = list(range(P, H)) + list(range(H + P, W))
+    for x, l in zip(free, single):
+        lanes[x] = dst[x] = l
+        sets[x] = (int(t.rl_den_ptr[l]), int(t.rl_den_ptr[l + 1]))
+    return lanes, dst, second, sets
+
+
+def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int = 0, split_den: int = 0) -> str:
+    """Complete HIP source of the specialised agent-per-wavefront kernel ``vk_dopri5_wspec``.
+
+    split_den = 1 lays the rate laws out two lanes per heavy denominator
+    (:func:`split_layout`): the padded denominator shape shrinks (C5: 6 sets x 3
+    members -> 4 x 3) and the kernel fits three waves per SIMD; the sum is the
+    table walk's, so results stay bit-identical."""
     sh = wave_shape(t)
     W = WAVE_LANES
     ns, nr, nl, nd = t.n_species, t.n_reactions, t.n_rate_laws, t.n_dyn
     if lds_ops >= 2 and ns + 1 > 32767:
         raise ValueError('lds_ops=2 keeps species indices in 16 bits')
     ny = nd + nr
+    lay = split_layout(t) if split_den else None
+    if split_den and (lay is None or lds_ops):
+        raise ValueError('split_den needs one round of <= 64 rate laws and lds_ops = 0')
+    SB = 0
+    if lay is not None:
+        lanes, dst, second, sets = lay
+        sh['SD'] = max(hi - lo for lo, hi in sets)
+        SB = max([hi - lo for (lo, hi), b in zip(sets, second) if b] or [0])
     LR, SN, MN, SD, MD = sh['LR'], sh['SN'], sh['MN'], sh['SD'], sh['MD']
     PAD_SP = ns   # cl[NS] == 1.0
     spn = [[[PAD_SP] * W for _ in range(max(SN * MN, 1))] for _ in range(LR)]
@@ -173,15 +224,18 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int
     enz = [[PAD_SP] * W for _ in range(LR)]
     spd = [[[PAD_SP] * W for _ in range(max(SD * MD, 1))] for _ in range(LR)]
     pid = [[[-1] * W for _ in range(max(SD * MD, 1))] for _ in range(LR)]
-    for l in range(nl):
-        r, lane = divmod(l, W)
+    if lay is None:
+        placement = [(l, divmod(l, W), (int(t.rl_den_ptr[l]), int(t.rl_den_ptr[l + 1]))) for l in range(nl)]
+    else:
+        placement = [(l, (0, x), sets[x]) for x, l in enumerate(lanes) if l >= 0]
+    for l, (r, lane), (dlo, dhi) in placement:
         enz[r][lane] = int(t.rl_enzyme[l])
         for si, s in enumerate(range(t.rl_num_ptr[l], t.rl_num_ptr[l + 1])):
             kc[r][si][lane] = int(t.rl_kcat[l])
             for mi, m in enumerate(range(t.set_ptr[s], t.set_ptr[s + 1])):
                 spn[r][si * MN + mi][lane] = int(t.mem_species[m])
                 pin[r][si * MN + mi][lane] = int(t.mem_param[m])
-        for si, s in enumerate(range(t.rl_den_ptr[l], t.rl_den_ptr[l + 1])):
+        for si, s in enumerate(range(dlo, dhi)):
             for mi, m in enumerate(range(t.set_ptr[s], t.set_ptr[s + 1])):
                 spd[r][si * MD + mi][lane] = int(t.mem_species[m])
                 pid[r][si * MD + mi][lane] = int(t.mem_param[m])
@@ -209,11 +263,13 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int
         _table('T_UI', 'int', ui), _table('T_UR', 'int', ur), _table('T_UC', 'double', uc),
         _table('T_RX', 'int', rx),
     ])
+    if lay is not None:
+        tables += '\n' + '\n'.join([_table('T_DST', 'int', [dst]), _table('T_SECOND', 'int', [second])])
     defs = '\n'.join('#define %s %d' % (k, v) for k, v in [
         ('NS', ns), ('ND', nd), ('NR', nr), ('NL', nl), ('NY', ny), ('LR', LR), ('SN', SN), ('MN', MN),
         ('SD', SD), ('MD', MD), ('NSLOT', NSLOT), ('UM', UM), ('RX_IDENTITY', sh['RX_IDENTITY']),
         ('RXR', RXR), ('RXM', RXM), ('TILE', ns + 1 + nr + 1 + nl + 1 + (W if pad_writes else 0)), ('WPE', wpe),
-        ('PAD_WRITES', int(pad_writes)), ('LDS_OPS', int(lds_ops))])
+        ('PAD_WRITES', int(pad_writes)), ('LDS_OPS', int(lds_ops)), ('SPLIT_DEN', int(lay is not None)), ('SB', SB)])
     umk = [max([int(t.upd_ptr[i + 1] - t.upd_ptr[i]) for i in range(k * W, min(nd, (k + 1) * W))] or [0])
            for k in range(NSLOT)]
     defs += '\n__device__ constexpr int UMK[NSLOT] = {%s};' % ', '.join(str(u) for u in umk)

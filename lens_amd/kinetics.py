@@ -47,13 +47,15 @@ class KineticsEngine:
 
         Afterwards :meth:`dopri5` defaults to variant 2 (straight-line rate
         laws, everything in VGPRs) instead of the generic table walk."""
-        from lens_amd.codegen import dopri5_source, wave_registers, wave_source
+        from lens_amd.codegen import dopri5_source, split_layout, wave_registers, wave_source
         if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:
             # too large for one lane: specialise the agent-per-wavefront kernel
             # instead, while its padded per-lane operands fit the register file
             if wave_registers(self.table) > self.WAVE_REGISTER_LIMIT:
                 return self
-            src = wave_source(self.table, self.WAVE_WAVES_PER_SIMD, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS)
+            split = int(bool(self.WAVE_SPLIT_DEN) and not self.WAVE_LDS_OPS and split_layout(self.table) is not None)
+            wpe = self.WAVE_WAVES_PER_SIMD or (3 if split else 2)
+            src = wave_source(self.table, wpe, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS, split)
         else:
             src = dopri5_source(self.table)
         with torch.cuda.device(self.device):
@@ -67,8 +69,12 @@ class KineticsEngine:
                                 # C5 113.5 -> 111.9 ms, profiles/r03/r03e_c5_probe.log)
     WAVE_LDS_OPS = 0            # 1: denominator 1/Km and stoichiometry read from LDS tables (fewer VGPRs);
                                 # 2: also the denominator member indices
-    WAVE_WAVES_PER_SIMD = 2     # occupancy the specialised wavefront kernel is compiled for: with its gathers
-                                # batched it needs 216 VGPRs (C5: 2 waves 120.5 ms; 3 waves spill, 224 ms)
+    WAVE_SPLIT_DEN = 1          # 1: the heaviest denominators split over lanes l and l + 32 (codegen.split_layout),
+                                # summed in set order (bit-identical); C5 112.0 -> 87.3 ms at 3 waves/SIMD
+                                # (profiles/r03/r03i_c5_probe.log)
+    WAVE_WAVES_PER_SIMD = None  # occupancy the specialised wavefront kernel is compiled for; None: 3 with split
+                                # denominators (190 -> 167 VGPRs, 16 spilled), else 2 (the batched gathers need
+                                # 216 VGPRs; C5: 2 waves 120.5 ms, 3 waves spill, 224 ms)
 
     def default_variant(self) -> int:
         if self.table.n_dyn + self.table.n_reactions > self.LANE_LIMIT:

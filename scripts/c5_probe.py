@@ -1,7 +1,7 @@
 """Time the agent-per-wavefront DP45 on the C5 network (50 species, 40 reactions):
 the table walk (variant 1) against the specialised kernel (variant 3), with and
 without branch-free LDS publishes (KineticsEngine.WAVE_PAD_WRITES) and LDS operand
-tables (WAVE_LDS_OPS) at 2 and 3 waves per SIMD.
+tables (WAVE_LDS_OPS), and split denominators (WAVE_SPLIT_DEN) at 2 and 3 waves per SIMD.
 
     python scripts/c5_probe.py [n_agents]
 """
@@ -19,14 +19,15 @@ print('ny', t.n_dyn + t.n_reactions, 'rate laws', t.n_rate_laws, 'F_rhs', t.flop
 params, conc = configs.heterogeneous_colony(t, cfg, n, sigma=0.2)
 P = torch.from_numpy(params).to(dev)
 m2c = torch.full((n,), 7e5, dtype=torch.float64, device=dev)
-cases = [('generic', 1, None, 1, 0), ('spec-2w', 3, 2, 1, 0), ('spec-2w-lds1', 3, 2, 1, 1), ('spec-3w-lds1', 3, 3, 1, 1),
-         ('spec-2w-lds2', 3, 2, 1, 2), ('spec-3w-lds2', 3, 3, 1, 2)]
-for label, variant, wpe, pad, lds in cases + cases[1:]:      # A/B/A/B in one process
+cases = [('generic', 1, None, 1, 0, 0), ('spec-2w', 3, 2, 1, 0, 0), ('spec-2w-split', 3, 2, 1, 0, 1),
+         ('spec-3w-split', 3, 3, 1, 0, 1), ('spec-3w-split-nopad', 3, 3, 0, 0, 1)]
+for label, variant, wpe, pad, lds, split in cases + cases[1:]:      # A/B/A/B in one process
     eng = KineticsEngine(t, dev)
     if wpe:
         eng.WAVE_WAVES_PER_SIMD = wpe
         eng.WAVE_PAD_WRITES = pad
         eng.WAVE_LDS_OPS = lds
+        eng.WAVE_SPLIT_DEN = split
         eng.specialize()
     C = torch.from_numpy(conc).to(dev)
     h = torch.zeros(n, dtype=torch.float64, device=dev)

@@ -62,8 +62,9 @@ def test_generated_rhs_matches_reference_fluxes(golden_fluxes):
             np.testing.assert_allclose(got, ref, rtol=1e-12, atol=1e-300)
 
 
-@pytest.mark.parametrize('wpe,pad,lds', [(2, 0, 0), (2, 1, 0), (3, 1, 1), (3, 1, 2)])
-def test_wave_source_compiles_for_gfx950(wpe, pad, lds, tmp_path):
+@pytest.mark.parametrize('wpe,pad,lds,split', [(2, 0, 0, 0), (2, 1, 0, 0), (3, 1, 1, 0), (3, 1, 2, 0), (2, 1, 0, 1),
+                                              (3, 0, 0, 1)])
+def test_wave_source_compiles_for_gfx950(wpe, pad, lds, split, tmp_path):
     """The agent-per-wavefront template (C5 network) in every option
     combination the engine can select: occupancy, branch-free publishes, LDS
     operand tables (levels 1 and 2).  hiprtc compiles the same text at run
@@ -71,4 +72,30 @@ def test_wave_source_compiles_for_gfx950(wpe, pad, lds, tmp_path):
     from lens_amd.codegen import wave_source
     cfg = configs.synthetic_network()
     t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
-    _hipcc_compile('#include <hip/hip_runtime.h>\n' + wave_source(t, wpe, pad, lds), tmp_path)
+    _hipcc_compile('#include <hip/hip_runtime.h>\n' + wave_source(t, wpe, pad, lds, split), tmp_path)
+
+
+def test_split_layout():
+    """codegen.split_layout on C5: the min(nl, 64 - nl) rate laws with the most
+    denominator sets take lanes l and l + 32, each half a contiguous run of
+    sets (first half ceil(n/2), summed in lane l); every rate law is written by
+    exactly one lane."""
+    from lens_amd.codegen import split_layout
+    cfg = configs.synthetic_network(n_species=50, n_reactions=40, n_enzymes=10)
+    t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
+    lanes, dst, second, sets = split_layout(t)
+    nl = t.n_rate_laws
+    assert sorted(d for d in dst if d >= 0) == list(range(nl))
+    nden = [int(t.rl_den_ptr[l + 1] - t.rl_den_ptr[l]) for l in range(nl)]
+    P = sum(second)
+    assert P == min(nl, 64 - nl)
+    for b in range(32, 64):
+        if second[b]:
+            a = b - 32
+            l = lanes[a]
+            assert lanes[b] == l and not second[a] and dst[a] == l and dst[b] == -1
+            assert sets[a][0] == int(t.rl_den_ptr[l]) and sets[a][1] == sets[b][0]
+            assert sets[b][1] == int(t.rl_den_ptr[l + 1]) and sets[a][1] - sets[a][0] == (nden[l] + 1) // 2
+    heavy = {lanes[b] for b in range(32, 64) if second[b]}
+    assert min(nden[l] for l in heavy) >= max([nden[l] for l in range(nl) if l not in heavy] or [0])
+    assert max(hi - lo for lo, hi in sets) == 4     # C5: 6 sets x 3 members -> 4 x 3

@@ -293,15 +293,19 @@ def _two_enzyme_network(n=96, seed=20261016):
     return cfg, t, params, conc
 
 
-@pytest.mark.parametrize('pad,lds', [(0, 0), (1, 0), (1, 1), (1, 2)])
+@pytest.mark.parametrize('pad,lds,split,wpe', [(0, 0, 0, 2), (1, 0, 0, 2), (1, 1, 0, 2), (1, 2, 0, 2), (1, 0, 1, 3),
+                                              (0, 0, 1, 3), (1, 0, 1, 2)])
 @pytest.mark.parametrize('net', ['c5', 'two_enzyme', 'wide'])
-def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad, lds):
+def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad, lds, split, wpe):
     """The specialised wavefront kernel (variant 3) against the table walk
     (variant 1): the padded identities are exact and everything else is the
     same arithmetic in the same order, so states, fluxes, counts, step counts
     and carried step sizes agree bit for bit -- with the branch-free LDS
-    publishes (pad = 1, padding lanes write a scratch slot) and the operand
-    tables in LDS (lds = 1) too."""
+    publishes (pad = 1, padding lanes write a scratch slot), the operand
+    tables in LDS (lds = 1, 2), and split denominators (split = 1: the second
+    half of a heavy rate law's sets computed in lane l + 32 and added by lane l
+    in set order; the 'wide' network has two rounds of rate laws, so the option
+    does not apply and the engine keeps one lane per rate law)."""
     from lens_amd import codegen
     if net == 'c5':
         cfg, t, params, conc = _big_network(n=300)
@@ -316,6 +320,8 @@ def test_dopri5_wave_spec_equals_generic_wave(dev, net, pad, lds):
     eng = _engine(t, dev)
     eng.WAVE_PAD_WRITES = pad
     eng.WAVE_LDS_OPS = lds
+    eng.WAVE_SPLIT_DEN = split
+    eng.WAVE_WAVES_PER_SIMD = wpe
     out = []
     for variant in (1, 3):
         if variant == 3:
