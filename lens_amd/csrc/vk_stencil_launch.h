@@ -19,4 +19,5 @@ void vk_launch_wl9(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 9 rows 
 void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS);        // as wl6 with streaming stores (k = 7, 9, 11)
 void vk_launch_wl6r(VK_STENCIL_LAUNCH_ARGS);         // wl6nt, stage 0 on the prefetch ring (k = 7, 9, 11)
 void vk_launch_wl6b(VK_STENCIL_LAUNCH_ARGS);         // wl6r with branch-free buffer stores (k = 7, 9, 11)
+void vk_launch_wl3b(VK_STENCIL_LAUNCH_ARGS);         // wl6b with 3 rows of lookahead (k = 7, 9, 11)
 void vk_launch_tb(VK_STENCIL_LAUNCH_ARGS);           // workgroup tile, LDS neighbour exchange

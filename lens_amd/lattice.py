@@ -43,7 +43,8 @@ def stencil_depth(k: int = 0) -> int:
 def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
     """Select the fused-pass kernel (0 = workgroup/LDS, 2/3/4 = wave/DPP lag-1 with 3/6/9
     prefetched rows, 6 = 3 with streaming stores, the default; 12 = 6 with stage 0 on the
-    prefetch ring, 13 = 12 with branch-free buffer stores) and output rows per tile
+    prefetch ring, 13 = 12 with branch-free buffer stores, 14 = 13 with 3 prefetched rows) and
+    output rows per tile
     (0 = auto; -1 keeps).  Other numbers are ignored (retired variants)."""
     native.load()
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
