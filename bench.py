@@ -96,7 +96,7 @@ def parse():
                    help='fma (default): tolerance mode, FMA-contracted passes within 1e-13 of the exact mode '
                         '(tests/test_stencil_modes.py); exact: bit-identical with scipy.ndimage.convolve')
     p.add_argument('--stencil-rows', type=int, default=None,
-                   help='output rows per wave tile (default: 64 for C4 on one GPU, else 0 = auto by band height '
+                   help='output rows per wave tile (default: 34 for C4 on one GPU, else 0 = auto by band height '
                         'and wave count)')
     p.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'],
                    help='nccl (= RCCL) for real runs; gloo stages through host memory (rehearsal only)')
@@ -399,8 +399,12 @@ def main():
     from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
     stencil_depth(args.stencil_depth)
     stencil_mode(args.stencil_mode)
-    if args.stencil_rows is None:   # 64-row tiles on the whole 4096^2 plane, else the auto rule (chunk_rows)
-        args.stencil_rows = 64 if (world == 1 and args.workload == 'c4') else 0
+    if args.stencil_rows is None:
+        # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of
+        # 3 waves x 1,024 SIMDs (64 rows: 4,864 waves, 1.58 rounds, 2.5-3 % slower per 100
+        # substeps, profiles/r03/r03h_stencil_rows_sweep.log, r03k_sweep.log); else the
+        # auto rule (chunk_rows)
+        args.stencil_rows = 34 if (world == 1 and args.workload == 'c4') else 0
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = balancer = None

@@ -264,7 +264,8 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int
         _table('T_RX', 'int', rx),
     ])
     if lay is not None:
-        tables += '\n' + '\n'.join([_table('T_DST', 'int', [dst]), _table('T_SECOND', 'int', [second])])
+        first = [1 if b < 32 and second[b + 32] else 0 for b in range(W)]
+        tables += '\n' + '\n'.join([_table('T_DST', 'int', [dst]), _table('T_FIRST', 'int', [first])])
     defs = '\n'.join('#define %s %d' % (k, v) for k, v in [
         ('NS', ns), ('ND', nd), ('NR', nr), ('NL', nl), ('NY', ny), ('LR', LR), ('SN', SN), ('MN', MN),
         ('SD', SD), ('MD', MD), ('NSLOT', NSLOT), ('UM', UM), ('RX_IDENTITY', sh['RX_IDENTITY']),
