@@ -1,0 +1,105 @@
+"""Generate tests/golden/kremling_ref.npz from the REFERENCE's own Kremling code
+(TEST FIXTURE GENERATOR; run here, where /root/reference exists -- the GPU box
+and the tests only read the committed .npz).
+
+vivarium/processes/Kremling2007_transport.py does not import in this container
+for ordinary reasons (its module imports vivarium.core and matplotlib; SURVEY.md
+§1.3).  Its model is self-contained, though, so this script reads the file's
+AST and evaluates only three pieces of it, unchanged, with numpy and scipy:
+
+* ``DEFAULT_PARAMETERS`` (:19-70), the dict expression evaluated without builtins;
+* the state key order, the keys of ``combined_state`` in ``next_update`` (:361-379);
+* ``model(state, t)``, the closure inside ``next_update`` (:220-351), compiled
+  as a module-level function whose free names ``p`` and ``state_keys`` are the
+  two above.
+
+With them it records, for 48 seeded states in each regime of the model's
+switch on internal G6P (> 0.01: G6P uptake; else lactose):
+
+* ``dy``: the reference right-hand side at every state;
+* ``end_tight`` / ``flux_tight``: odeint (LSODA) of the reference ``model``
+  over the reference's own grid ``np.arange(0, 1/3600, 0.01/3600)`` (:354-357,
+  :384) at rtol 1e-13 / atol 1e-16 -- the last row (internal species, :409) and
+  the mean of the flux integrals (:404), for 12 of the states;
+* ``end_default``: the same call at odeint's default tolerances, i.e. the
+  reference's literal call.
+
+No reference source is copied into the repository: the file is parsed at
+generation time only.
+
+    python tests/golden/make_kremling_ref.py
+"""
+
+from __future__ import annotations
+
+import ast
+import os
+import sys
+
+import numpy as np
+from scipy.integrate import odeint
+
+REF = '/root/reference/vivarium/processes/Kremling2007_transport.py'
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'kremling_ref.npz')
+
+
+def _pieces(path):
+    tree = ast.parse(open(path).read(), path)
+    params = keys = model = None
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and any(getattr(t, 'id', None) == 'DEFAULT_PARAMETERS' for t in node.targets):
+            params = eval(compile(ast.Expression(node.value), path, 'eval'), {'__builtins__': {}})
+        if isinstance(node, ast.ClassDef) and node.name == 'Transport':
+            nu = next(f for f in node.body if isinstance(f, ast.FunctionDef) and f.name == 'next_update')
+            model = next(f for f in nu.body if isinstance(f, ast.FunctionDef) and f.name == 'model')
+            for st in nu.body:
+                if isinstance(st, ast.Assign) and getattr(st.targets[0], 'id', None) == 'combined_state':
+                    keys = [k.value for k in st.value.keys]
+    assert params and keys and model, 'reference layout changed'
+    mod = ast.Module(body=[model], type_ignores=[])
+    ns = {'np': np, 'p': dict(params), 'state_keys': list(keys)}
+    exec(compile(mod, path, 'exec'), ns)
+    return ns['model'], params, keys
+
+
+def main():
+    model, params, keys = _pieces(REF)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    from oracle import kremling as ok
+    assert tuple(keys) == ok.STATE_KEYS, keys
+    rng = np.random.default_rng(2026_10_17)
+    states = []
+    for regime, (internal, external) in enumerate(((ok.GLC_G6P_INTERNAL, ok.GLC_G6P_EXTERNAL),
+                                                   (ok.GLC_LCT_SHIFT_INTERNAL, ok.GLC_LCT_SHIFT_EXTERNAL))):
+        s0 = ok.initial_state(internal, external)
+        for i in range(48):
+            s = s0.copy()
+            if i:
+                s[:8] *= rng.uniform(0.6, 1.4, 8)
+                s[8:11] *= rng.uniform(0.5, 1.5, 3)
+                s[11:] = rng.uniform(0.0, 1e-3, 4) if i % 2 else 0.0
+            if regime:       # the lactose branch: internal G6P at or below the 0.01 switch (:245)
+                s[4] = 0.01 * (rng.uniform(0.1, 1.0) if i else 0.5)
+                s[2] = max(s[2], 1e-5 * rng.uniform(0.5, 2.0))   # some LACZ to take up lactose
+            states.append(s)
+    states = np.array(states)                                     # [96, 15]
+    dy = np.array([model(s, 0.0) for s in states])
+    t = np.arange(0, 1.0 / 3600, 0.01 / 3600)
+    pick = np.r_[0:6, 48:54]                                      # 6 states per regime
+    end_tight, flux_tight, end_default = [], [], []
+    for i in pick:
+        s = states[i].copy()
+        s[11:] = 0.0                                             # next_update starts the integrals at 0 (:375-378)
+        sol = odeint(model, s, t, rtol=1e-13, atol=1e-16, mxstep=500000)
+        end_tight.append(sol[-1, :8])
+        flux_tight.append([np.mean(sol[:, c]) for c in range(11, 15)])     # per column, as :404
+        end_default.append(odeint(model, s, t)[-1, :8])
+    np.savez_compressed(OUT, states=states, dy=dy, pick=pick, end_tight=np.array(end_tight),
+                        flux_tight=np.array(flux_tight), end_default=np.array(end_default),
+                        keys=np.array(keys), params=np.array([params[k] for k in sorted(params)], dtype=np.float64),
+                        param_names=np.array(sorted(params)))
+    print('wrote', OUT, states.shape, 'regimes', int((states[:, 4] > 0.01).sum()), int((states[:, 4] <= 0.01).sum()))
+
+
+if __name__ == '__main__':
+    main()

@@ -2,12 +2,20 @@
 
 Oracle: oracle/kremling.py -- the restated RHS integrated by scipy odeint on
 the reference's 100-point grid.  The reference holds no fixture for this
-process (its test only runs it), so parity is against odeint here: tight
-odeint (rtol 1e-13) as truth, and the literal reference call (odeint's
-default tolerances).  Bar (north star): |gpu - odeint| <= 1e-6 * |odeint|
+process (its test only runs it).  The restatement is pinned to the
+reference's own code by tests/golden/kremling_ref.npz
+(tests/golden/make_kremling_ref.py evaluates the reference file's
+DEFAULT_PARAMETERS and its ``model`` closure, unchanged, in both regimes of
+the G6P switch, and integrates that ``model`` with odeint on the reference's
+grid): the oracle's RHS equals the reference's bit for bit, and the GPU
+kernel's end states are checked against the reference model's odeint.  Truth
+is tight odeint (rtol 1e-13); the literal reference call uses odeint's
+default tolerances.  Bar (north star): |gpu - odeint| <= 1e-6 * |odeint|
 + 1e-12 per species; fluxes likewise; exchange counts equal to +-1 (counts
 truncate a concentration difference, so a last-digit difference can flip an
 integer boundary)."""
+
+import os
 
 import numpy as np
 import pytest
@@ -31,6 +39,37 @@ def test_params_layout_matches_reference_names():
         assert lk.KREMLING_PARAMETERS[name] == ok.DEFAULT_PARAMETERS[name]
     from lens_amd import native
     assert all(f in lk.KREMLING_PARAMETERS for f, _ in native.VkKremlingParams._fields_)
+
+
+GOLDEN = os.path.join(os.path.dirname(__file__), 'golden', 'kremling_ref.npz')
+
+
+def test_oracle_rhs_equals_reference_model():
+    """oracle.kremling.rhs == the reference's own model(state, t) (evaluated
+    from Kremling2007_transport.py:220-351 by make_kremling_ref.py), bit for
+    bit, at 96 states across both regimes of the internal-G6P switch; and the
+    restated DEFAULT_PARAMETERS are the reference's."""
+    z = np.load(GOLDEN)
+    assert tuple(z['keys']) == ok.STATE_KEYS
+    assert dict(zip(z['param_names'], z['params'])) == {k: float(v) for k, v in ok.DEFAULT_PARAMETERS.items()}
+    states = z['states']
+    assert (states[:, 4] > 0.01).sum() == 48 and (states[:, 4] <= 0.01).sum() == 48
+    got = np.array([ok.rhs(st, 0.0, ok.DEFAULT_PARAMETERS) for st in states])
+    assert np.array_equal(got, z['dy'])
+
+
+def test_oracle_step_equals_reference_odeint():
+    """oracle.kremling.step (odeint of the restated RHS) against odeint of the
+    reference model on the same grid and tolerances: identical RHS, so the
+    same LSODA path."""
+    z = np.load(GOLDEN)
+    for j, i in enumerate(z['pick']):
+        s = z['states'][i].copy()
+        s[11:] = 0.0
+        internal, fluxes, _, _ = ok.step(s, rtol=1e-13, atol=1e-16)
+        assert np.array_equal(internal, z['end_tight'][j])
+        assert np.array_equal(fluxes, z['flux_tight'][j])
+        assert np.array_equal(ok.step(s)[0], z['end_default'][j])
 
 
 @pytest.fixture(scope='module')
@@ -80,6 +119,30 @@ def test_gpu_kremling_matches_odeint(dev, condition):
             err_ref = np.abs(lit - internal)
             assert np.all(err_gpu <= np.maximum(1e-6 * np.abs(internal) + 1e-12, err_ref)), (err_gpu, err_ref)
         states[:8] = got[:8]     # internal := last row; external held (environment owns it)
+
+
+@pytest.mark.gpu
+def test_gpu_kremling_vs_reference_model_odeint(dev):
+    """One GPU step from each of 12 fixture states (6 per regime) against odeint
+    of the reference's own model (kremling_ref.npz): internal species and mean
+    fluxes within the north-star 1e-6, and at least as close to the tight
+    solution as the reference's literal (default-tolerance) call."""
+    from lens_amd.kremling import KremlingColony
+    z = np.load(GOLDEN)
+    states = z['states'][z['pick']].T.copy()          # [15, 12]
+    n = states.shape[1]
+    col = KremlingColony(n, device=dev)
+    col.set_state(states[:11])
+    col.step(1.0)
+    col.check_status()
+    got = col.state.cpu().numpy()[:8]
+    flux = col.flux.cpu().numpy()
+    for a in range(n):
+        ref, fref, lit = z['end_tight'][a], z['flux_tight'][a], z['end_default'][a]
+        assert _close(got[:, a], ref), (a, got[:, a], ref)
+        assert _close(flux[:, a], fref), (a, flux[:, a], fref)
+        err_gpu, err_ref = np.abs(got[:, a] - ref), np.abs(lit - ref)
+        assert np.all(err_gpu <= np.maximum(1e-6 * np.abs(ref) + 1e-12, err_ref)), (a, err_gpu, err_ref)
 
 
 @pytest.mark.gpu
