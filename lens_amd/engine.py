@@ -89,6 +89,12 @@ class Experiment:
         self._ports: Dict[int, Tuple] = {}          # id(process) -> (process, its port names)
         self._updater_cache: Dict[Tuple, str] = {}  # resolved schema updater per leaf path
         self._leaf_updaters: Dict[Tuple, Dict] = {}  # branch path -> {leaf key: updater name}
+        # (process path, port) -> (structure version, parent node, parent path, key): the
+        # store node a port resolves to.  Value updates replace leaves only; the version
+        # moves whenever a dict-valued node is replaced or the schema registers nodes, and
+        # an entry from an older version is resolved again.
+        self._port_nodes: Dict[Tuple, Tuple] = {}
+        self._version = 0
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -127,6 +133,7 @@ class Experiment:
     def _register(self, path, schema):
         if not isinstance(schema, dict):
             return
+        self._version += 1
         self._updater_cache.clear()
         self._leaf_updaters.clear()
         keys = [k for k in schema if not k.startswith('_')]
@@ -168,13 +175,25 @@ class Experiment:
             entry = self._ports[id(proc)] = (proc, tuple(proc.ports_schema()))
         return entry[1]
 
+    def _port_node(self, proc_path, port):
+        key = (proc_path, port)
+        ent = self._port_nodes.get(key)
+        if ent is None or ent[0] != self._version:
+            path = self.port_path(proc_path, port)
+            ent = self._port_nodes[key] = (self._version, self.get(path[:-1]), path[:-1], path[-1])
+        return ent
+
     def process_states(self, path, proc):
-        return {port: self.get(self.port_path(path, port)) for port in self._port_names(proc)}
+        out = {}
+        for port in self._port_names(proc):
+            ent = self._port_node(path, port)
+            out[port] = ent[1][ent[3]]
+        return out
 
     def apply_update(self, update, proc_path):
         for port, value in update.items():
-            path = self.port_path(proc_path, port)
-            self._apply(self.get(path[:-1]), path[:-1], path[-1], value, proc_path)
+            _, parent, ppath, key = self._port_node(proc_path, port)
+            self._apply(parent, ppath, key, value, proc_path)
 
     def _apply(self, parent, ppath, key, update, proc_path):
         # parent = the store node at ppath holding `key` (branches pass their own node
@@ -200,7 +219,9 @@ class Experiment:
                 name = names.get(k)                                      # a plain leaf, inlined
                 if name is None:
                     name = names[k] = self._updater_at(cpath + (k,))
-                current[k] = updaters[name](cur, value, None)
+                new = current[k] = updaters[name](cur, value, None)
+                if type(new) is dict:
+                    self._version += 1
             return
         states = None
         if inline:
@@ -208,7 +229,10 @@ class Experiment:
             name, mapping = (spec, None) if isinstance(spec, str) else (spec['updater'], spec.get('port_mapping'))
             value = update.get('_value')
             if mapping is not None:
-                states = {up: self.get(self.port_path(proc_path, pp)) for up, pp in mapping.items()}
+                states = {}
+                for up, pp in mapping.items():
+                    ent = self._port_node(proc_path, pp)
+                    states[up] = ent[1][ent[3]]
         else:
             names = self._leaf_updaters.get(ppath)
             if names is None:
@@ -217,7 +241,9 @@ class Experiment:
             if name is None:
                 name = names[key] = self._updater_at(ppath + (key,))
             value = update
-        parent[key] = self.updaters[name](current, value, states)
+        new = parent[key] = self.updaters[name](current, value, states)
+        if isinstance(current, dict) or isinstance(new, dict):
+            self._version += 1          # a branch was replaced: cached port nodes below it are stale
 
     def send_updates(self, updates, derivers=None):
         for update, path in updates:
