@@ -21,8 +21,8 @@ switch on internal G6P (> 0.01: G6P uptake; else lactose):
   over the reference's own grid ``np.arange(0, 1/3600, 0.01/3600)`` (:354-357,
   :384) at rtol 1e-13 / atol 1e-16 -- the last row (internal species, :409) and
   the mean of the flux integrals (:404), for 12 of the states;
-* ``end_default``: the same call at odeint's default tolerances, i.e. the
-  reference's literal call.
+* ``end_default`` / ``flux_default``: the same call at odeint's default
+  tolerances, i.e. the reference's literal call.
 
 No reference source is copied into the repository: the file is parsed at
 generation time only.
@@ -86,16 +86,19 @@ def main():
     dy = np.array([model(s, 0.0) for s in states])
     t = np.arange(0, 1.0 / 3600, 0.01 / 3600)
     pick = np.r_[0:6, 48:54]                                      # 6 states per regime
-    end_tight, flux_tight, end_default = [], [], []
+    end_tight, flux_tight, end_default, flux_default = [], [], [], []
     for i in pick:
         s = states[i].copy()
         s[11:] = 0.0                                             # next_update starts the integrals at 0 (:375-378)
         sol = odeint(model, s, t, rtol=1e-13, atol=1e-16, mxstep=500000)
         end_tight.append(sol[-1, :8])
         flux_tight.append([np.mean(sol[:, c]) for c in range(11, 15)])     # per column, as :404
-        end_default.append(odeint(model, s, t)[-1, :8])
+        lit = odeint(model, s, t)
+        end_default.append(lit[-1, :8])
+        flux_default.append([np.mean(lit[:, c]) for c in range(11, 15)])
     np.savez_compressed(OUT, states=states, dy=dy, pick=pick, end_tight=np.array(end_tight),
                         flux_tight=np.array(flux_tight), end_default=np.array(end_default),
+                        flux_default=np.array(flux_default),
                         keys=np.array(keys), params=np.array([params[k] for k in sorted(params)], dtype=np.float64),
                         param_names=np.array(sorted(params)))
     print('wrote', OUT, states.shape, 'regimes', int((states[:, 4] > 0.01).sum()), int((states[:, 4] <= 0.01).sum()))
