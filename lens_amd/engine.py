@@ -94,6 +94,7 @@ class Experiment:
         # moves whenever a dict-valued node is replaced or the schema registers nodes, and
         # an entry from an older version is resolved again.
         self._port_nodes: Dict[Tuple, Tuple] = {}
+        self._plans: Dict[Tuple, Tuple] = {}        # process path -> (version, process, kinetics plan)
         self._version = 0
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
@@ -245,9 +246,92 @@ class Experiment:
         if isinstance(current, dict) or isinstance(new, dict):
             self._version += 1          # a branch was replaced: cached port nodes below it are stale
 
+    def _kinetics_plan(self, proc_path, process):
+        """Where a BatchedConvenienceKinetics update lands, resolved once per
+        (process path, structure version): per output its store node, key and
+        updater -- what apply_update finds by walking the update dict that
+        unpack_update would build (internal deltas, fluxes, then the fields'
+        inline update_field_with_exchange).  None when a target is not a plain
+        leaf (the generic path handles it)."""
+        ent = self._plans.get(proc_path)
+        if ent is not None and ent[0] == self._version and ent[1] is process:
+            return ent[2]
+        t = process.table
+        plan = None
+        try:
+            def leaves(port, names):
+                _, parent, ppath, key = self._port_node(proc_path, port)
+                node = parent.get(key, _MISSING)
+                if node is _MISSING:
+                    return [None] * len(names)           # no such port: apply_update skips it
+                if not isinstance(node, dict):
+                    raise LookupError
+                cpath = ppath + (key,)
+                out = []
+                for k in names:
+                    cur = node.get(k, _MISSING)
+                    if cur is _MISSING:
+                        out.append(None)                 # no such leaf: the update is dropped
+                    elif isinstance(cur, dict):
+                        raise LookupError
+                    else:
+                        out.append((node, k, self.updaters[self._updater_at(cpath + (k,))]))
+                return out
+            dyn = [leaves(port, [name])[0] for port, name in t.species[:t.n_dyn]]
+            flux = leaves('fluxes', t.reaction_ids)
+            _, fparent, fppath, fkey = self._port_node(proc_path, 'fields')
+            fnode = fparent.get(fkey, _MISSING)
+            if not isinstance(fnode, dict):
+                raise LookupError                        # the generic path decides
+            states = {}
+            for up, pp in {'global': 'global', 'dimensions': 'dimensions'}.items():
+                e = self._port_node(proc_path, pp)
+                states[up] = e[1][e[3]]
+            exch = self.updaters['update_field_with_exchange']
+            fields = []
+            for mol in t.external_ids:
+                cur = fnode.get(mol, _MISSING)
+                if isinstance(cur, dict):
+                    raise LookupError
+                fields.append(None if cur is _MISSING else (fnode, mol))
+            plan = (dyn, flux, fields, exch, states)
+        except (LookupError, KeyError, TypeError):
+            plan = None
+        self._plans[proc_path] = (self._version, process, plan)
+        return plan
+
+    def _apply_kinetics(self, proc_path, process, fluxes, deltas, counts):
+        plan = self._kinetics_plan(proc_path, process)
+        if plan is None:
+            self.apply_update(process.unpack_update(fluxes, deltas, counts), proc_path)
+            return
+        dyn, flux, fields, exch, states = plan
+        bump = False
+        for tgt, d in zip(dyn, deltas):
+            if tgt is not None:
+                node, k, fn = tgt
+                new = node[k] = fn(node[k], d, None)
+                bump |= type(new) is dict
+        for tgt, f in zip(flux, fluxes):
+            if tgt is not None:
+                node, k, fn = tgt
+                new = node[k] = fn(node[k], np.float64(f), None)
+                bump |= type(new) is dict
+        for tgt, c in zip(fields, counts):
+            if tgt is not None:
+                node, mol = tgt
+                new = node[mol] = exch(node[mol], c, states)
+                bump |= isinstance(new, dict)
+        if bump:
+            self._version += 1
+
     def send_updates(self, updates, derivers=None):
         for update, path in updates:
-            self.apply_update(update.get(), path)
+            raw = getattr(update, 'raw', None)
+            if raw is not None:
+                self._apply_kinetics(path, *raw())       # BatchedInvoke: no update dict
+            else:
+                self.apply_update(update.get(), path)
         if derivers is None:
             derivers = [(p, s) for p, s in self._walk(self.processes, ()) if s.is_deriver()]
         for path, deriver in derivers:

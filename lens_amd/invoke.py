@@ -46,7 +46,7 @@ class _Packed:
         self.conc, self.m2c = process.pack_state(states)    # species values as a list, m2c
 
 
-def _run_group(items: List[_Packed], device=None) -> List[dict]:
+def _run_group(items: List[_Packed], device=None, raw: bool = False) -> List:
     p0 = items[0].process
     t = p0.table
     eng = engine_for(p0, device)
@@ -80,6 +80,8 @@ def _run_group(items: List[_Packed], device=None) -> List[dict]:
     flux_l = flux.t().cpu().tolist()
     delta_l = delta.t().cpu().tolist()
     counts_l = counts.t().cpu().tolist()
+    if raw:
+        return [(it.process, f, d, c) for it, f, d, c in zip(items, flux_l, delta_l, counts_l)]
     return [it.process.unpack_update(f, d, c) for it, f, d, c in zip(items, flux_l, delta_l, counts_l)]
 
 
@@ -104,7 +106,14 @@ class _Future:
         self.slot = slot
 
     def get(self, timeout=0):
+        """The reference's update dict (convenience_kinetics.py:316-349)."""
         return self.owner._result(self.slot)
+
+    def raw(self):
+        """(process, fluxes, deltas, counts) -- the same outputs before they are
+        packed into the update dict; lens_amd.engine.Experiment applies them
+        straight into the store (same updaters, same order)."""
+        return self.owner._raw(self.slot)
 
 
 class _Immediate:
@@ -141,11 +150,15 @@ class BatchedInvoke:
             key = (it.process.signature, it.interval, it.process.parameters.get('integrator', 'euler'))
             groups.setdefault(key, []).append((slot, it))
         for members in groups.values():
-            res = _run_group([it for _, it in members], self.device)
+            res = _run_group([it for _, it in members], self.device, raw=True)
             for (slot, _), r in zip(members, res):
                 self._results[slot] = r
 
-    def _result(self, slot):
+    def _raw(self, slot):
         if slot not in self._results:
             self.flush()
         return self._results.pop(slot)
+
+    def _result(self, slot):
+        process, f, d, c = self._raw(slot)
+        return process.unpack_update(f, d, c)

@@ -134,3 +134,76 @@ def test_c1_both_loops_bitwise():
         assert a.state[port] == b.state[port]
     for m in a.state['fields']:
         assert np.array_equal(a.state['fields'][m], b.state['fields'][m])
+
+
+class _FakeKineticsInvoke:
+    """An invoke hook that returns seeded kinetics outputs for every
+    BatchedConvenienceKinetics call, either as a future with ``raw()`` (the
+    path BatchedInvoke takes in lens_amd.engine) or with ``get()`` only (the
+    reference's protocol: the update dict of unpack_update)."""
+
+    class _F:
+        def __init__(self, out, with_raw):
+            self.out = out
+            if with_raw:
+                self.raw = lambda: self.out
+
+        def get(self, timeout=0):
+            p, f, d, c = self.out
+            return p.unpack_update(f, d, c)
+
+    def __init__(self, with_raw, seed=5):
+        self.with_raw = with_raw
+        self.rng = np.random.default_rng(seed)
+
+    def __call__(self, process, interval, states):
+        from lens_amd.process import BatchedConvenienceKinetics
+        if not isinstance(process, BatchedConvenienceKinetics):
+            out = process.next_update(interval, states)
+            return type('I', (), {'get': lambda self, timeout=0: out})()
+        t = process.table
+        out = (process, self.rng.normal(size=t.n_reactions).tolist(), self.rng.normal(size=t.n_dyn).tolist(),
+               self.rng.integers(-50, 50, size=t.n_ext).tolist())
+        return self._F(out, self.with_raw)
+
+
+def test_direct_kinetics_apply_equals_update_dict():
+    """engine.Experiment applies a BatchedInvoke result straight into the store
+    (_apply_kinetics: cached store nodes and updaters) instead of building and
+    walking the update dict.  Against the dict path on CPU -- seeded outputs,
+    6 agents, host fields (the reference's update_field_with_exchange
+    arithmetic), a missing flux leaf and 3 steps -- the stores are identical,
+    value and type."""
+    from lens_amd.process import BatchedConvenienceKinetics
+    cfg = configs.glc_lct_config()
+    states = []
+    for with_raw in (True, False):
+        procs, topo, agents = {'agents': {}}, {'agents': {}}, {}
+        for a in range(6):
+            aid = 'a%d' % a
+            procs['agents'][aid] = {'kinetics': BatchedConvenienceKinetics(dict(cfg, time_step=1.0))}
+            topo['agents'][aid] = {'kinetics': {
+                'internal': ('internal',), 'external': ('boundary', 'external'), 'fluxes': ('fluxes',),
+                'fields': ('..', '..', 'fields'), 'dimensions': ('..', '..', 'dimensions'), 'global': ('boundary',)}}
+            agents[aid] = {'internal': dict(cfg['initial_state']['internal']), 'fluxes': {},
+                           'boundary': {'location': [0.5 + a, 1.5], 'mmol_to_counts': 1e6 * (a + 1),
+                                        'external': dict(cfg['initial_state']['external'])}}
+        init = {'agents': agents, 'dimensions': {'bounds': [8.0, 4.0], 'n_bins': [8, 4], 'depth': 3.0},
+                'fields': {m: np.ones((8, 4)) for m in cfg['initial_state']['external']}}
+        exp = Experiment({'processes': procs, 'topology': topo, 'initial_state': init,
+                          'invoke': _FakeKineticsInvoke(with_raw)})
+        del exp.state['agents']['a3']['fluxes'][sorted(exp.state['agents']['a3']['fluxes'])[0]]
+        exp.update(3.0)
+        if with_raw:
+            assert len(exp._plans) == 6 and all(e[2] is not None for e in exp._plans.values())
+        states.append(exp.state)
+
+    def same(x, y):
+        if isinstance(x, dict):
+            return isinstance(y, dict) and list(x) == list(y) and all(same(x[k], y[k]) for k in x)
+        if isinstance(x, np.ndarray):
+            return isinstance(y, np.ndarray) and np.array_equal(x, y)
+        return type(x) is type(y) and (x == y or (x != x and y != y))
+
+    assert same(states[0], states[1])
+    assert not np.array_equal(states[0]['fields']['glc__D_e'], np.ones((8, 4)))     # the exchange landed
