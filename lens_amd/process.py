@@ -177,11 +177,21 @@ class BatchedConvenienceKinetics(ProcessBase):
     def pack_state(self, states):
         """One agent's species values (table order) and its mmol_to_counts, as
         Python floats."""
-        vals = []
-        for port, name in self.table.species:
-            v = states.get(port)
-            v = v.get(name, 0.0) if isinstance(v, dict) else 0.0
-            vals.append(float(getattr(v, 'magnitude', v)))
+        groups = self.__dict__.get('_pack_groups')
+        if groups is None:          # species grouped by port, in table order within each
+            by_port = {}
+            for i, (port, name) in enumerate(self.table.species):
+                by_port.setdefault(port, []).append((i, name))
+            groups = self._pack_groups = list(by_port.items())
+            self._n_species = len(self.table.species)
+        vals = [0.0] * self._n_species
+        for port, members in groups:
+            d = states.get(port)
+            if isinstance(d, dict):
+                get = d.get
+                for i, name in members:
+                    v = get(name, 0.0)
+                    vals[i] = v if type(v) is float else float(getattr(v, 'magnitude', v))
         return vals, float(_magnitude(states['global']['mmol_to_counts']))
 
     def unpack_update(self, fluxes, deltas, counts):
