@@ -129,9 +129,14 @@ def wave_shape(t: RateLawTable) -> dict:
     }
 
 
-def wave_registers(t: RateLawTable) -> int:
-    """Rough VGPR estimate of the specialised wave kernel (lane constants + DP45 state)."""
+def wave_registers(t: RateLawTable, split: bool = False) -> int:
+    """Rough VGPR estimate of the specialised wave kernel (lane constants + DP45 state);
+    ``split``: with the split-denominator layout (:func:`split_layout`).  It runs ~30
+    under the compiler's count (C5: 180 / 220 one lane per rate law, 162 / 190 split)."""
     s = wave_shape(t)
+    lay = split_layout(t) if split else None
+    if lay is not None:
+        s['SD'] = max(hi - lo for lo, hi in lay[3])
     lane = s['LR'] * (3 * s['SN'] * s['MN'] + 2 * s['SN'] + 1 + 3 * s['SD'] * s['MD']) + s['NSLOT'] * (1 + 3 * s['UM'])
     return lane + 18 * s['NSLOT'] + 40
 
@@ -175,6 +180,8 @@ def split_layout(t: RateLawTable):
         return None
     nden = [int(t.rl_den_ptr[l + 1] - t.rl_den_ptr[l]) for l in range(nl)]
     P = min(nl, W - nl, H)
+    if P == 0:
+        return None            # 64 rate laws: no lane to spare
     order = sorted(range(nl), key=lambda l: (-nden[l], l))
     heavy = sorted(order[:P])
     single = sorted(order[P:])

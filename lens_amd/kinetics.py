@@ -54,7 +54,9 @@ class KineticsEngine:
             if wave_registers(self.table) > self.WAVE_REGISTER_LIMIT:
                 return self
             split = int(bool(self.WAVE_SPLIT_DEN) and not self.WAVE_LDS_OPS and split_layout(self.table) is not None)
-            wpe = self.WAVE_WAVES_PER_SIMD or (3 if split else 2)
+            # 3 waves per SIMD where the split layout's estimate leaves room (C5: 162 -> 167
+            # VGPRs, 16 spilled, 0.63 VALU busy); larger networks keep 2
+            wpe = self.WAVE_WAVES_PER_SIMD or (3 if split and wave_registers(self.table, True) <= 165 else 2)
             src = wave_source(self.table, wpe, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS, split)
         else:
             src = dopri5_source(self.table)
