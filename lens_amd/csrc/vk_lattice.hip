@@ -79,7 +79,9 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // 6 = variant 3 with streaming stores (the default), 12 = variant 6 with stage 0 reading the
 // prefetch ring (no per-group copies of in-flight rows, no vmcnt(0) per group), 13 = variant 12
 // with branch-free buffer stores (exact vmcnt bookkeeping: PD rows of lookahead), 14 = 13 with
-// PD = 3 (a ring of 6 rows, variant 6's unroll and code size).
+// PD = 3 (a ring of 6 rows, variant 6's unroll and code size), 15 = variant 6 with zigzag chunks
+// (workgroups down a column tile, odd chunks bottom-up in the tolerance mode: shared halo rows
+// read by both neighbours at about the same time).
 // Retired after A/B on the GPU:
 // 1 (lag-2 wave tile), 5 (4 waves/SIMD cap, spills), 7 (streaming loads), and the round-2
 // experiments 8-11 (four columns per lane, compact boundary body, split stages, LDS-crossbar
@@ -88,7 +90,7 @@ static int g_stencil_kernel = 6;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 0 || (variant >= 2 && variant <= 4) || variant == 6 || (variant >= 12 && variant <= 14))
+    if (variant == 0 || (variant >= 2 && variant <= 4) || variant == 6 || (variant >= 12 && variant <= 15))
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
@@ -179,8 +181,10 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform, 0);
         } else if (g_stencil_kernel >= 12 && (k == 7 || k == 9 || k == 11)) {
-            auto launch = g_stencil_kernel == 14 ? vk_launch_wl3b : (g_stencil_kernel == 13 ? vk_launch_wl6b
-                                                                                             : vk_launch_wl6r);
+            auto launch = g_stencil_kernel == 15   ? vk_launch_wl6z
+                          : g_stencil_kernel == 14 ? vk_launch_wl3b
+                          : g_stencil_kernel == 13 ? vk_launch_wl6b
+                                                   : vk_launch_wl6r;
             launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
                    coeff_dt, uniform);
         } else if ((g_stencil_kernel == 6 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11)) {

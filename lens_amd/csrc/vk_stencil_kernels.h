@@ -182,9 +182,17 @@ struct WtLane {
     int cA;              // this lane's first column (cB = cA + 1)
     int ny;
     uint32_t voff;       // VK_WL_BUF_STORE: byte offset of column A in its row, out of range (store dropped) if not wA
+    bool rev;            // VK_WL_ZIGZAG: this wave walks its chunk bottom-up (physical row = m - logical row)
+    int m;
     bool wA, wB;         // writes its column A / B
     bool lA, rA, lB, rB; // reflect flags (EDGE tiles only)
 };
+
+// Physical row of logical row x, clamped into the pass's input rows [lo, hi).
+__device__ __forceinline__ int64_t wl_row(const WtLane &L, int x, int lo, int hi) {
+    const int r = L.rev ? L.m - x : x;
+    return (int64_t)min(max(r, lo), hi - 1);
+}
 
 template <bool EDGE>
 __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t row_off, const WtLane &L) {
@@ -242,10 +250,10 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     if constexpr (WL_RING) {
         // row j lives in slot (j - i0) mod NR; U = (i - i0) mod NR.  Row i+PD goes
         // to the slot of row i-3, whose last use (as stage 0's up row) was iteration i-1
-        pf[(U + PD) % NR] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L);
+        pf[(U + PD) % NR] = wt_load<EDGE>(s, wl_row(L, i + PD, in_lo, in_hi) * ny, L);
     } else {
         FR[0] = pf[U];                                                                      // row i
-        pf[U] = wt_load<EDGE>(s, (int64_t)min(max(i + PD, in_lo), in_hi - 1) * ny, L); // row i+PD
+        pf[U] = wt_load<EDGE>(s, wl_row(L, i + PD, in_lo, in_hi) * ny, L);             // row i+PD
     }
     const int r_out = i - K;
     const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
@@ -287,7 +295,8 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
             FR[q + 1] = v;
         } else if (row_ok) {
             if (FINAL && !FAST) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
-            double *o = d + (int64_t)r_out * ny + L.cA;
+            const int64_t r_phys = L.rev ? L.m - r_out : r_out;
+            double *o = d + r_phys * ny + L.cA;
             if (!EDGE) {
 #ifdef VK_WL_BUF_STORE
                 // Branch-free store: lanes that do not write carry an out-of-range
@@ -299,7 +308,7 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
                 (void)o;
                 typedef int i4v __attribute__((ext_vector_type(4)));
                 const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)(d + (int64_t)r_out * ny), 0, (int)(ny * 8), 0x00020000);
+                    (void *)(d + r_phys * ny), 0, (int)(ny * 8), 0x00020000);
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v), rs, (int)L.voff, 0, 2);
 #else
                 if (L.wA) wl_store(o, v);
@@ -368,10 +377,10 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
     // (ring: slots NR-2 and NR-1)
     double2 &w_up = WL_RING ? pf[NR - 2] : S0[0];
     double2 &w_cn = WL_RING ? pf[NR - 1] : S1[0];
-    w_up = wt_load<EDGE>(s, (int64_t)min(max(i0 - 2, in_lo), in_hi - 1) * ny, L);
-    w_cn = wt_load<EDGE>(s, (int64_t)min(max(i0 - 1, in_lo), in_hi - 1) * ny, L);
+    w_up = wt_load<EDGE>(s, wl_row(L, i0 - 2, in_lo, in_hi) * ny, L);
+    w_cn = wt_load<EDGE>(s, wl_row(L, i0 - 1, in_lo, in_hi) * ny, L);
 #pragma unroll
-    for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, (int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny, L);
+    for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, wl_row(L, i0 + u, in_lo, in_hi) * ny, L);
 #pragma unroll
     for (int u = 0; u < 3; ++u)   // FINAL: base rows of the first 3 output rows (i0 - K + u)
         gp[u] = FINAL && !FAST && (L.wA || L.wB)
@@ -397,8 +406,17 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int lane = threadIdx.x & 63;
     if (wave >= tiles_x * chunks_y * n_fields) return;
+#ifdef VK_WL_ZIGZAG
+    // the 4 waves of a workgroup take 4 vertically adjacent chunks of one column
+    // tile, odd chunks walked bottom-up: each chunk boundary's halo rows are then
+    // read by both neighbours at about the same time (both at their start or both
+    // at their end), mostly on one CU
+    const int ty = wave % chunks_y;
+    const int tx = (wave / chunks_y) % tiles_x;
+#else
     const int tx = wave % tiles_x;
     const int ty = (wave / tiles_x) % chunks_y;
+#endif
     const int f = wave / (tiles_x * chunks_y);
     if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;
     const int c0 = out_lo + ty * rows_per_chunk;
@@ -406,6 +424,8 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     const int x0 = tx * W;
     WtLane L;
     L.ny = ny;
+    L.rev = false;
+    L.m = 0;
     L.cA = x0 - KH + 2 * lane;
     const int cB = L.cA + 1;
     L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
@@ -422,6 +442,12 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
                       (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
                       (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
     const double c4 = 1.0 - 4.0 * coef;      // FAST only
+#ifdef VK_WL_ZIGZAG
+    // only the tolerance mode: (N + S) + (E + W) is symmetric in N and S, so a
+    // bottom-up walk gives the same bits (the exact mode's order is not)
+    L.rev = FAST && !edge && (ty & 1);
+    L.m = c0 + c1 - 1;
+#endif
     if (edge)
         diffuse_wl_body<K, PD, true, FINAL, FAST>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef,
                                                   c4);

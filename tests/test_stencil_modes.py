@@ -53,7 +53,7 @@ def _rel(got, ref):
     return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-300))
 
 
-@pytest.mark.parametrize('variant', [6, 12, 13, 14])
+@pytest.mark.parametrize('variant', [6, 12, 13, 14, 15])
 @pytest.mark.parametrize('depth', [7, 9, 11])
 def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
     from lens_amd.lattice import Lattice
@@ -71,7 +71,7 @@ def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
                 assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))
 
 
-@pytest.mark.parametrize('variant', [6, 12, 13, 14])
+@pytest.mark.parametrize('variant', [6, 12, 13, 14, 15])
 @pytest.mark.parametrize('depth,rows', [(9, 64), (7, 40), (11, 48), (9, 17)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
 def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape, variant):
