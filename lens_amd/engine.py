@@ -96,6 +96,7 @@ class Experiment:
         self._port_nodes: Dict[Tuple, Tuple] = {}
         self._plans: Dict[Tuple, Tuple] = {}        # process path -> (version, process, kinetics plan)
         self._version = 0
+        self._state_seen = None
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -352,6 +353,9 @@ class Experiment:
                 gc.enable()
 
     def _update(self, interval):
+        if self.state is not self._state_seen:     # the whole store was replaced from outside
+            self._state_seen = self.state
+            self._version += 1
         time = 0
         front = {}
         # the reference re-walks the tree every iteration (:1373-1380) because a
