@@ -108,11 +108,16 @@ extern "C" int vk_set_stencil_mode(int32_t mode) {
     return prev;
 }
 
-static int g_stencil_depth = 9;   // max substeps per HBM pass (odd; 1 = one launch per substep)
+// max substeps per HBM pass: odd, 1 = one launch per substep; or 10, which plans a
+// tolerance-mode whole step of a multiple of 10 substeps as 10-deep passes (three
+// buffers: the field itself is free once the first pass has read it), other calls
+// as depth 9
+static int g_stencil_depth = 9;
 
 extern "C" int vk_set_stencil_depth(int32_t k) {
     const int prev = g_stencil_depth;
-    if (k >= 1 && k <= 15) g_stencil_depth = k | 1;
+    if (k == 10) g_stencil_depth = 10;
+    else if (k >= 1 && k <= 15) g_stencil_depth = k | 1;
     return prev;
 }
 
@@ -151,7 +156,30 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
     const int bot_reflect = edge_bot ? hi_max - 1 : 0x7fffffff;
     hipStream_t s = (hipStream_t)stream;
     const int last_in_call = sub_begin + sub_count - 1;
+    if (g_stencil_depth == 10 && g_stencil_mode == 1 && sub_begin == 0 && sub_count == n_sub && n_sub % 10 == 0 &&
+        n_sub >= 20 && work1) {
+        // Tolerance mode, whole step, 10 k substeps: k passes of 10.  The final pass
+        // writes the field without reading it back (no f0), so the field is a third
+        // buffer: pass p reads `cur` and writes the work buffer it did not read, and the
+        // last pass writes the field.  Uniform planes skip every pass and keep their field.
+        const double *cur = field;
+        for (int j = 0, p = 0; j < n_sub; j += 10, ++p) {
+            const int e = j + 9;
+            const int grow = last_in_call - e;
+            const int lo = max(lo_min, row_lo - grow);
+            const int hi = min(hi_max, row_hi + grow);
+            const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
+            double *dst = (e == n_sub - 1) ? field : (cur == work0 ? work1 : work0);
+            vk_launch_wl6nt(10, s, cur, dst, nullptr, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                            bot_reflect, coeff_dt, uniform);
+            int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
+            if (rc) return rc;
+            cur = dst;
+        }
+        return VK_OK;
+    }
     int depth = g_stencil_depth | 1;   // odd
+    if (g_stencil_depth == 10) depth = 9;
     if (depth > 15) depth = 15;
     // Pass plan: the fewest odd depths <= depth that sum to sub_count (a sum of
     // P odd numbers has the parity of P), as even as possible -- e.g. 100 =

@@ -19,4 +19,6 @@ void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS) {
         vk_nt::launch<9, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
     else if (k == 11)
         vk_nt::launch<11, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
+    else if (k == 10)   // tolerance mode only; 3 rows prefetched keep it at 154 VGPRs (3 waves per SIMD)
+        vk_nt::launch_fast<10, 3>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
 }

@@ -54,7 +54,7 @@ def _rel(got, ref):
 
 
 @pytest.mark.parametrize('variant', [6, 12, 13, 14, 15])
-@pytest.mark.parametrize('depth', [7, 9, 11])
+@pytest.mark.parametrize('depth', [7, 9, 10, 11])
 def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
     from lens_amd.lattice import Lattice
     z = np.load(os.path.join(GOLDEN, 'stencil.npz'))
@@ -72,7 +72,7 @@ def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
 
 
 @pytest.mark.parametrize('variant', [6, 12, 13, 14, 15])
-@pytest.mark.parametrize('depth,rows', [(9, 64), (7, 40), (11, 48), (9, 17)])
+@pytest.mark.parametrize('depth,rows', [(9, 64), (7, 40), (11, 48), (9, 17), (10, 34), (10, 17), (10, 64)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
 def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape, variant):
     from lens_amd.lattice import Lattice
@@ -87,6 +87,28 @@ def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape, variant):
     cpu.diffuse(ref, 5.0 * 0.01, 100)
     assert _rel(got, ref) < TOL
     assert not np.array_equal(got, f0)
+
+
+def test_depth10_full_c4_planes_vs_depth9(dev):
+    """The tolerance mode's 10-deep whole-step plan (10 passes per 100 substeps,
+    three buffers) against the 9-deep plan on the full 4096^2 x 2 planes, three
+    steps (1e-13), and a plane that is uniform stays bit for bit."""
+    from lens_amd import configs
+    from lens_amd.lattice import Lattice
+    n = 4096
+    glc = configs.gaussian_bump_field((n, n))
+    out = {}
+    for depth in (9, 10):
+        with _mode('fma', depth, 34):
+            lat = Lattice(['glc__D_e', 'ac_e'], (n, n), (float(n), float(n)), 10.0, 5.0, device=dev,
+                          initial={'glc__D_e': glc, 'ac_e': np.full((n, n), 0.25)})
+            for _ in range(3):
+                lat.diffuse(1.0)
+            torch.cuda.synchronize()
+            out[depth] = lat
+    a, b = out[9].fields[0], out[10].fields[0]
+    assert float((a - b).abs().max() / a.abs().max()) < TOL
+    assert torch.equal(out[10].fields[1], torch.full_like(out[10].fields[1], 0.25))
 
 
 def test_fma_mode_full_c4_planes_vs_exact_mode(dev):
