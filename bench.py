@@ -66,6 +66,8 @@ def stencil_kernel_name(variant, depth, mode='exact'):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
     if mode == 'fma' and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
+    if mode == 'fma' and depth == 10:
+        return 'vk_nt::k_diffuse_wl<10, 3, false, true>'
     if variant == 0:
         return 'k_diffuse_tb<%d>' % depth
     if variant == 6:
