@@ -95,7 +95,7 @@ def parse():
                         '6 = 3 with streaming stores (default)')
     p.add_argument('--stencil-depth', type=int, default=None,
                    help='substeps fused per HBM pass (odd, or 10: tolerance-mode whole steps as 10-deep passes); '
-                        'default 10 for C4 on one GPU in the fma mode, else 9')
+                        'default 10 for C4 in the fma mode, else 9')
     p.add_argument('--stencil-mode', default='fma', choices=['fma', 'exact'],
                    help='fma (default): tolerance mode, FMA-contracted passes within 1e-13 of the exact mode '
                         '(tests/test_stencil_modes.py); exact: bit-identical with scipy.ndimage.convolve')
@@ -405,7 +405,9 @@ def main():
         # 100 substeps as 10 passes of 10 instead of 8 x 9 + 4 x 7: -2.3 % per 100 substeps,
         # -3 % per step (profiles/r03/r03v/); the 10-deep pass keeps the 9-deep pass's column
         # halo (KH = 10)
-        args.stencil_depth = 10 if (world == 1 and args.workload == 'c4' and args.stencil_mode == 'fma') else 9
+        # (row bands too: a middle rank's step at N = 2 / 4 / 8 runs 0.968 / 0.610 / 0.432 ms
+        # against 0.995 / 0.628 / 0.450 at depth 9, profiles/r03/r03x_rank_emulate.log)
+        args.stencil_depth = 10 if (args.workload == 'c4' and args.stencil_mode == 'fma') else 9
     stencil_depth(args.stencil_depth)
     stencil_mode(args.stencil_mode)
     if args.stencil_rows is None:
