@@ -520,6 +520,45 @@ def test_banded_diffusion_equals_whole(dev):
         assert np.array_equal(got, whole.owned('a').cpu().numpy()), (world, halo)
 
 
+def test_banded_depth10_plan_equals_whole(dev):
+    """The tolerance mode's 10-deep whole-step plan on row bands with one
+    100-deep halo block per step (the C4 bench at N > 1) equals the whole plane
+    under the same plan bit for bit: the same cells, the same arithmetic."""
+    from lens_amd import native
+    from lens_amd.distributed import row_bands
+    from lens_amd.lattice import Lattice, stencil_depth, stencil_mode
+    rng = np.random.default_rng(4)
+    nx, ny = 300, 237
+    f0 = rng.random((nx, ny)) * 5
+    prev_m, prev_d = stencil_mode('fma'), stencil_depth(10)
+    try:
+        whole = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+        whole.diffuse(1.0)
+        for world in (2, 3):
+            bands = row_bands(nx, world)
+            lats = [Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                            row_band=b, halo=100, initial={'a': f0}) for b in bands]
+            for r, lat in enumerate(lats):          # the one halo exchange of the step
+                if not lat.edge_top:
+                    nb = lats[r - 1]
+                    lat.fields[:, lat.row_lo - 100:lat.row_lo].copy_(nb.fields[:, nb.row_hi - 100:nb.row_hi])
+                if not lat.edge_bot:
+                    nb = lats[r + 1]
+                    lat.fields[:, lat.row_hi:lat.row_hi + 100].copy_(nb.fields[:, nb.row_lo:nb.row_lo + 100])
+            for lat in lats:
+                lo_min = lat.row_lo if lat.edge_top else 0
+                hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
+                native.check(native._lib.vk_diffuse(
+                    native.ptr(lat.fields), native.ptr(lat.work0), native.ptr(lat.work1), 1,
+                    lat.field_stride, ny, lat.row_lo, lat.row_hi, lo_min, hi_max, int(lat.edge_top),
+                    int(lat.edge_bot), 0, 100, 100, lat.diffusion * 0.01, 0, native.stream_handle()), 'diffuse')
+            got = torch.cat([lat.owned('a') for lat in lats], 0).cpu().numpy()
+            assert np.array_equal(got, whole.owned('a').cpu().numpy()), world
+    finally:
+        stencil_mode(prev_m)
+        stencil_depth(prev_d)
+
+
 def test_lattice_colony_side_stream_overlap_is_exact(dev):
     """Kinetics + gather on the side stream beside the diffusion passes gives
     the same fields and agent state, bit for bit, as the one-stream order."""
