@@ -78,7 +78,9 @@ def stencil_kernel_name(variant, depth, mode='exact'):
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=10)
+    p.add_argument('--steps', type=int, default=None,
+                   help='timed steps (default 10; C2, whose replayed step is ~5 us, 200 so that the timed '
+                        'region is not the barrier and synchronisation around it)')
     p.add_argument('--warmup', type=int, default=3)
     p.add_argument('--workload', default='c4', choices=sorted(WORKLOADS))
     p.add_argument('--integrator', default='dopri5', choices=['dopri5', 'euler'])
@@ -115,7 +117,10 @@ def parse():
                         'reported as untimed_settle_steps')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
-    return p.parse_args()
+    args = p.parse_args()
+    if args.steps is None:
+        args.steps = 200 if args.workload == 'c2' else 10
+    return args
 
 
 def settle_steps_needed(warmup_s: float, warmup_steps: int, settle_ms: float, cap: int = 2000) -> int:
