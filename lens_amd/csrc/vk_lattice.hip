@@ -97,9 +97,10 @@ extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
 }
 
 // 0 = bit-exact with scipy.ndimage.convolve (the default), 1 = tolerance mode: the
-// variant-6 passes with FMA-contracted arithmetic (5 FP64 ops per cell-substep
-// instead of 6) and no base re-read in the final pass; fields agree with the exact
-// mode to ~1e-14 relative (tests/test_stencil_modes.py)
+// variant-6 passes with FMA-contracted arithmetic on a rescaled field (4 FP64 ops
+// per cell-substep instead of 6, vk_stencil_kernels.h) and no base re-read in the
+// final pass; fields agree with the exact mode to ~1e-14 relative
+// (tests/test_stencil_modes.py)
 int g_stencil_mode = 0;
 
 extern "C" int vk_set_stencil_mode(int32_t mode) {

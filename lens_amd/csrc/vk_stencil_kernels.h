@@ -229,7 +229,7 @@ constexpr bool WL_RING = false;
 #endif
 
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool STEADY, int U>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, bool STEADY, int U>
 __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[wl_ring(PD)], double2 (&gp)[3],
                                         const double *__restrict__ s, double *d,
                                         const double *g, const WtLane &L, int i, int c0, int c1,
@@ -280,9 +280,18 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
             rightB = L.rB ? cen.y : rightB;
         }
         double2 v;
-        if (FAST) {
+        if (FAST && SC) {
+            // scaled tolerance mode: stage q carries the field divided by c4^q
+            // (c4 = 1 - 4coef), so c4*c + coef*sum becomes t + (coef/c4)*sum -- 4 FP64
+            // ops per cell; the last stage multiplies c4^K back in.  Here coef holds
+            // coef/c4 and c4 holds c4^K (diffuse_wl_tile)
+            const double sA = (up.x + dn.x) + (leftA + rightA);
+            const double sB = (up.y + dn.y) + (leftB + rightB);
+            v = make_double2(fma(coef, sA, cen.x), fma(coef, sB, cen.y));
+            if (q + 1 == K) v = make_double2(c4 * v.x, c4 * v.y);
+        } else if (FAST) {
             // tolerance mode: c + coef*(N+S+E+W-4c) = fma(coef, (N+S)+(E+W), (1-4coef)*c),
-            // 5 FP64 ops per cell instead of 6 (coef holds (coef, 1-4coef) packed by the caller)
+            // 5 FP64 ops per cell instead of 6
             const double sA = (up.x + dn.x) + (leftA + rightA);
             const double sB = (up.y + dn.y) + (leftB + rightB);
             v = make_double2(fma(coef, sA, c4 * cen.x), fma(coef, sB, c4 * cen.y));
@@ -321,20 +330,20 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     }
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool STEADY, int U0, int... Us>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
                                          double2 (&pf)[wl_ring(PD)], double2 (&gp)[3], const double *__restrict__ s, double *d,
                                          const double *g, const WtLane &L, int i, int c0, int c1,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
                                          double c4) {
-    wl_iter<K, PD, EDGE, FINAL, FAST, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi,
+    wl_iter<K, PD, EDGE, FINAL, FAST, SC, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi,
                                                   top_reflect, bot_reflect, coef, c4);
     if constexpr (sizeof...(Us) > 0)
-        wl_group<K, PD, EDGE, FINAL, FAST, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo,
+        wl_group<K, PD, EDGE, FINAL, FAST, SC, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo,
                                                           in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, int... Us>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
                                                 double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[wl_ring(PD)], double2 (&gp)[3],
                                                 const double *__restrict__ s, double *d,
@@ -346,23 +355,23 @@ __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...
 #define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4
     constexpr int NU = wl_ring(PD);                  // iterations per unrolled group
     int i = i0;
-    for (; i + NU <= i1 && i < s_lo; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);   // fill
+    for (; i + NU <= i1 && i < s_lo; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, false, Us...>(WL_ARGS);   // fill
 #ifdef VK_WL_BUF_STORE
     // enter the steady loop with no memory operation in flight, so that the
     // compiler's wait counts at its header come from the loop's own (branch-free)
     // iterations and not from the fill phase's conditional stores
     if (!EDGE) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 #endif
-    for (; i + NU - 1 <= s_hi; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, true, Us...>(WL_ARGS);          // steady
-    for (; i + NU <= i1; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, false, Us...>(WL_ARGS);               // drain
+    for (; i + NU - 1 <= s_hi; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, true, Us...>(WL_ARGS);          // steady
+    for (; i + NU <= i1; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, false, Us...>(WL_ARGS);               // drain
     // tail: fewer than NU iterations, phases 0.. in order
-    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, FAST, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1,
+    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, FAST, SC, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1,
                                                               in_lo, in_hi, top_reflect, bot_reflect, coef, c4)
                   : void()), ...);
 #undef WL_ARGS
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST>
+template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC>
 __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
@@ -386,7 +395,7 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
         gp[u] = FINAL && !FAST && (L.wA || L.wB)
                     ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
                     : make_double2(0.0, 0.0);
-    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST>(std::make_integer_sequence<int, NR>(), S0, S1, S2, pf, gp, s, d, g, L,
+    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST, SC>(std::make_integer_sequence<int, NR>(), S0, S1, S2, pf, gp, s, d, g, L,
                                               c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
@@ -448,12 +457,29 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     L.rev = FAST && !edge && (ty & 1);
     L.m = c0 + c1 - 1;
 #endif
+    if constexpr (FAST) {
+        // the scaled form while c4^-K stays far from overflow (|c4| >= 1e-3, i.e.
+        // coef not within 2.5e-4 of 1/4; coef = 0 gives the identity exactly)
+        if (fabs(c4) >= 1e-3) {
+            const double q = coef / c4;
+            double cK = 1.0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) cK *= c4;
+            if (edge)
+                diffuse_wl_body<K, PD, true, FINAL, FAST, true>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect,
+                                                                bot_reflect, q, cK);
+            else
+                diffuse_wl_body<K, PD, false, FINAL, FAST, true>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect,
+                                                                 bot_reflect, q, cK);
+            return;
+        }
+    }
     if (edge)
-        diffuse_wl_body<K, PD, true, FINAL, FAST>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef,
-                                                  c4);
+        diffuse_wl_body<K, PD, true, FINAL, FAST, false>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect,
+                                                         coef, c4);
     else
-        diffuse_wl_body<K, PD, false, FINAL, FAST>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef,
-                                                   c4);
+        diffuse_wl_body<K, PD, false, FINAL, FAST, false>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect,
+                                                          bot_reflect, coef, c4);
 }
 
 // Aliasing: the FINAL pass writes the field it also reads as the base plane
