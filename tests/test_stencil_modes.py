@@ -4,8 +4,9 @@ The default mode is bit-identical with the reference's
 ``f += coef * scipy.ndimage.convolve(f, LAP, mode='reflect')``
 (vivarium/processes/diffusion_field.py:385-394; tests/test_gpu_parity.py).
 The tolerance mode contracts each cell-substep into
-``fma(coef, (N+S)+(E+W), (1-4coef)*C)`` and writes the final pass without the
-delta-then-accumulate re-read.  Bar: within 1e-13 relative (of the plane's
+``fma(coef/c4, (N+S)+(E+W), C)`` on a field carried rescaled by c4^-stage
+(c4 = 1 - 4coef; ``fma(coef, (N+S)+(E+W), c4*C)`` when |c4| < 1e-3) and writes
+the final pass without the delta-then-accumulate re-read.  Bar: within 1e-13 relative (of the plane's
 largest value) of the scipy goldens and of the exact mode after whole steps,
 at every tile geometry; uniform planes still skipped exactly.
 """
@@ -134,3 +135,43 @@ def test_fma_mode_full_c4_planes_vs_exact_mode(dev):
         rel = float((a - b).abs().max() / a.abs().max())
         assert rel < TOL, (f, rel)
         assert not torch.equal(a, b)        # the modes do differ (in the last bits)
+
+
+@pytest.mark.parametrize('depth,n_sub', [(10, 20), (9, 18)])
+@pytest.mark.parametrize('coef', [0.05, 0.2497, 0.2498, 0.25])
+def test_fma_mode_scaled_and_unscaled_forms_vs_c_oracle(dev, depth, n_sub, coef):
+    """The tolerance mode carries the field rescaled by c4^-stage (c4 = 1 - 4coef)
+    while |c4| >= 1e-3 and keeps the unscaled fma form nearer coef = 1/4: both
+    sides of that cut (0.2497 scaled, 0.2498 and 0.25 unscaled) on a ragged
+    plane with edge tiles, against the C oracle (1e-13)."""
+    from lens_amd import native
+    rng = np.random.default_rng(11)
+    nx, ny = 333, 517
+    f0 = rng.random((nx, ny)) + 0.5
+    with _mode('fma', depth, 17):
+        field = torch.tensor(f0, device=dev)
+        w0, w1 = torch.empty_like(field), torch.empty_like(field)
+        native.check(native._lib.vk_diffuse(
+            native.ptr(field), native.ptr(w0), native.ptr(w1), 1, nx * ny, ny, 0, nx, 0, nx, 1, 1,
+            0, n_sub, n_sub, coef, 0, native.stream_handle()), 'diffuse')
+        got = field.cpu().numpy()
+    ref = np.ascontiguousarray(f0.copy())
+    cpu.diffuse(ref, coef, n_sub)
+    assert _rel(got, ref) < TOL, _rel(got, ref)
+    assert not np.array_equal(got, f0)
+
+
+def test_fma_mode_zero_coefficient_is_identity(dev):
+    """coef = 0 (no diffusion): the scaled form is t + 0 * sum with c4^K = 1, so
+    the field comes back bit for bit."""
+    from lens_amd import native
+    rng = np.random.default_rng(12)
+    nx, ny = 300, 237
+    f0 = rng.random((nx, ny)) * 5
+    with _mode('fma', 10, 17):
+        field = torch.tensor(f0, device=dev)
+        w0, w1 = torch.empty_like(field), torch.empty_like(field)
+        native.check(native._lib.vk_diffuse(
+            native.ptr(field), native.ptr(w0), native.ptr(w1), 1, nx * ny, ny, 0, nx, 0, nx, 1, 1,
+            0, 20, 20, 0.0, 0, native.stream_handle()), 'diffuse')
+        assert np.array_equal(field.cpu().numpy(), f0)
