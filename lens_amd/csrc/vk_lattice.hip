@@ -81,7 +81,8 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // with branch-free buffer stores (exact vmcnt bookkeeping: PD rows of lookahead), 14 = 13 with
 // PD = 3 (a ring of 6 rows, variant 6's unroll and code size), 15 = variant 6 with zigzag chunks
 // (workgroups down a column tile, odd chunks bottom-up in the tolerance mode: shared halo rows
-// read by both neighbours at about the same time).
+// read by both neighbours at about the same time), 16 = variant 6 with 6 rows prefetched
+// in the tolerance mode's 10-deep passes (2 waves per SIMD).
 // Retired after A/B on the GPU:
 // 1 (lag-2 wave tile), 5 (4 waves/SIMD cap, spills), 7 (streaming loads), and the round-2
 // experiments 8-11 (four columns per lane, compact boundary body, split stages, LDS-crossbar
@@ -90,7 +91,7 @@ static int g_stencil_kernel = 6;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 0 || (variant >= 2 && variant <= 4) || variant == 6 || (variant >= 12 && variant <= 15))
+    if (variant == 0 || (variant >= 2 && variant <= 4) || variant == 6 || (variant >= 12 && variant <= 16))
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
@@ -171,8 +172,9 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             const int hi = min(hi_max, row_hi + grow);
             const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
             double *dst = (e == n_sub - 1) ? field : (cur == work0 ? work1 : work0);
-            vk_launch_wl6nt(10, s, cur, dst, nullptr, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
-                            bot_reflect, coeff_dt, uniform);
+            (g_stencil_kernel == 16 ? vk_launch_wl6nt10p6 : vk_launch_wl6nt)(
+                10, s, cur, dst, nullptr, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
+                coeff_dt, uniform);
             int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
             if (rc) return rc;
             cur = dst;
@@ -184,8 +186,9 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         // convention gives the state after substep 9): the bench's single-pass timing
         const int grow = last_in_call - 9;
         const int lo = max(lo_min, row_lo - grow), hi = min(hi_max, row_hi + grow);
-        vk_launch_wl6nt(10, s, field, work1, nullptr, n_fields, field_stride, ny, lo, hi, max(lo_min, lo - 10),
-                        min(hi_max, hi + 10), top_reflect, bot_reflect, coeff_dt, uniform);
+        (g_stencil_kernel == 16 ? vk_launch_wl6nt10p6 : vk_launch_wl6nt)(
+            10, s, field, work1, nullptr, n_fields, field_stride, ny, lo, hi, max(lo_min, lo - 10),
+            min(hi_max, hi + 10), top_reflect, bot_reflect, coeff_dt, uniform);
         return vk::launch_check("vk_diffuse kernel (depth 10)");
     }
     int depth = g_stencil_depth | 1;   // odd
@@ -218,14 +221,15 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform, 0);
-        } else if (g_stencil_kernel >= 12 && (k == 7 || k == 9 || k == 11)) {
+        } else if (g_stencil_kernel >= 12 && g_stencil_kernel <= 15 && (k == 7 || k == 9 || k == 11)) {
             auto launch = g_stencil_kernel == 15   ? vk_launch_wl6z
                           : g_stencil_kernel == 14 ? vk_launch_wl3b
                           : g_stencil_kernel == 13 ? vk_launch_wl6b
                                                    : vk_launch_wl6r;
             launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
                    coeff_dt, uniform);
-        } else if ((g_stencil_kernel == 6 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11)) {
+        } else if ((g_stencil_kernel == 6 || g_stencil_kernel == 16 || g_stencil_mode == 1) &&
+                   (k == 7 || k == 9 || k == 11)) {
             vk_launch_wl6nt(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
                             bot_reflect, coeff_dt, uniform);
         } else if (g_stencil_kernel >= 2) {

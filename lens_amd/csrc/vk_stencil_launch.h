@@ -20,5 +20,6 @@ void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS);        // as wl6 with streaming st
 void vk_launch_wl6r(VK_STENCIL_LAUNCH_ARGS);         // wl6nt, stage 0 on the prefetch ring (k = 7, 9, 11)
 void vk_launch_wl6b(VK_STENCIL_LAUNCH_ARGS);         // wl6r with branch-free buffer stores (k = 7, 9, 11)
 void vk_launch_wl3b(VK_STENCIL_LAUNCH_ARGS);         // wl6b with 3 rows of lookahead (k = 7, 9, 11)
-void vk_launch_wl6z(VK_STENCIL_LAUNCH_ARGS);         // wl6nt with zigzag chunks (k = 7, 9, 11)
+void vk_launch_wl6z(VK_STENCIL_LAUNCH_ARGS);
+void vk_launch_wl6nt10p6(VK_STENCIL_LAUNCH_ARGS);   // 10-deep fma pass, 6 rows prefetched (variant 16)         // wl6nt with zigzag chunks (k = 7, 9, 11)
 void vk_launch_tb(VK_STENCIL_LAUNCH_ARGS);           // workgroup tile, LDS neighbour exchange
