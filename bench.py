@@ -64,18 +64,19 @@ SPLIT_STEPS = 6            # eager steps timed for the kinetics / diffusion spli
 
 def stencil_kernel_name(variant, depth, mode='exact'):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
+    if mode == 'fma' and variant >= 20 and depth <= 11:
+        pd = {21: 2, 22: 6}.get(variant, 4) if depth in (9, 10) else 4
+        return 'vk_ps::k_diffuse_ps<%d, %d, 2, true>' % (depth, pd)
     if mode == 'fma' and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
     if mode == 'fma' and depth == 10:
         return 'vk_nt::k_diffuse_wl<10, 3, false, true>'
-    if variant == 0:
-        return 'k_diffuse_tb<%d>' % depth
-    if variant == 6:
+    if variant in (6, 20, 21, 22) and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false>' % depth
-    return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 * (variant - 1))
+    return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 if variant == 2 else 6)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=None,
@@ -92,9 +93,10 @@ def parse():
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=6,
-                   help='0 workgroup/LDS, 2/3/4 wave/DPP lag-1 prefetch 3/6/9 rows, '
-                        '6 = 3 with streaming stores (default)')
+    p.add_argument('--stencil-kernel', type=int, default=20,
+                   help='tolerance mode: 20 = pair-sum passes (default), 21 / 22 = 2 / 6 rows prefetched, '
+                        '6 = the variant-6 FMA form; exact mode: 2 / 3 = wave tiles prefetching 3 / 6 rows, '
+                        '6 (and 20-22) = 3 with streaming stores')
     p.add_argument('--stencil-depth', type=int, default=None,
                    help='substeps fused per HBM pass (odd, or 10: tolerance-mode whole steps as 10-deep passes); '
                         'default 10 for C4 in the fma mode, else 9')
@@ -117,10 +119,31 @@ def parse():
                         'reported as untimed_settle_steps')
     p.add_argument('--no-cpu-baseline', action='store_true')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
-    args = p.parse_args()
+    args = p.parse_args(argv)
     if args.steps is None:
         args.steps = 200 if args.workload == 'c2' else 10
     return args
+
+
+def stencil_settings(args, world):
+    """(mode, depth, kernel, rows) of the fused passes for this run -- what the
+    bench times, and what tests/test_configs.py checks at full size."""
+    depth = args.stencil_depth
+    if depth is None:
+        # 100 substeps as 10 passes of 10 instead of 8 x 9 + 4 x 7: -2.3 % per 100 substeps,
+        # -3 % per step (profiles/r03/r03v/); the 10-deep pass keeps the 9-deep pass's column
+        # halo (KH = 10)
+        # (row bands too: a middle rank's step at N = 2 / 4 / 8 runs 0.968 / 0.610 / 0.432 ms
+        # against 0.995 / 0.628 / 0.450 at depth 9, profiles/r03/r03x_rank_emulate.log)
+        depth = 10 if (args.workload == 'c4' and args.stencil_mode == 'fma') else 9
+    rows = args.stencil_rows
+    if rows is None:
+        # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of
+        # 3 waves x 1,024 SIMDs (64 rows: 4,864 waves, 1.58 rounds, 2.5-3 % slower per 100
+        # substeps, profiles/r03/r03h_stencil_rows_sweep.log, r03k_sweep.log); else the
+        # auto rule (chunk_rows)
+        rows = 34 if (world == 1 and args.workload == 'c4') else 0
+    return args.stencil_mode, depth, args.stencil_kernel, rows
 
 
 def settle_steps_needed(warmup_s: float, warmup_steps: int, settle_ms: float, cap: int = 2000) -> int:
@@ -406,21 +429,9 @@ def main():
             dist.destroy_process_group()
         return
     from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
-    if args.stencil_depth is None:
-        # 100 substeps as 10 passes of 10 instead of 8 x 9 + 4 x 7: -2.3 % per 100 substeps,
-        # -3 % per step (profiles/r03/r03v/); the 10-deep pass keeps the 9-deep pass's column
-        # halo (KH = 10)
-        # (row bands too: a middle rank's step at N = 2 / 4 / 8 runs 0.968 / 0.610 / 0.432 ms
-        # against 0.995 / 0.628 / 0.450 at depth 9, profiles/r03/r03x_rank_emulate.log)
-        args.stencil_depth = 10 if (args.workload == 'c4' and args.stencil_mode == 'fma') else 9
+    args.stencil_mode, args.stencil_depth, args.stencil_kernel, args.stencil_rows = stencil_settings(args, world)
     stencil_depth(args.stencil_depth)
     stencil_mode(args.stencil_mode)
-    if args.stencil_rows is None:
-        # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of
-        # 3 waves x 1,024 SIMDs (64 rows: 4,864 waves, 1.58 rounds, 2.5-3 % slower per 100
-        # substeps, profiles/r03/r03h_stencil_rows_sweep.log, r03k_sweep.log); else the
-        # auto rule (chunk_rows)
-        args.stencil_rows = 34 if (world == 1 and args.workload == 'c4') else 0
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     halo_ex = allred = balancer = None

@@ -200,35 +200,39 @@ class Colony:
         if self.n and (int(ix.min()) < lat.row_lo_global or int(ix.max()) >= lat.row_hi_global):
             raise ValueError('agents outside this rank\'s row band: attach a distributed.AgentRouter '
                              '(division moves daughters across band edges)')
-        self.occ = occupancy(self.bin_lin, self.n)
+        self.occ = occupancy(self.bin_lin, self.n, getattr(self, 'agent_order', None))
         self._layout += 1            # captured graphs hold the old occupancy buffers
 
     def sort_by_bin(self):
-        """Store the agents in bin order (a stable sort: agents sharing a bin keep
-        their relative order), so that the exchange scatter and the gather read
-        the per-agent arrays and the lattice as streams instead of scattered
-        lines.  Every result is unchanged: the exchange adds a bin's agents in
-        the same order (the reference's agent order), and agents do not
+        """Store the agents in bin order, so that the exchange scatter and the
+        gather read the per-agent arrays and the lattice as streams instead of
+        scattered lines.  The sort key is (bin, reference order): agents sharing
+        a bin stay in the reference's relative order, and the exchange
+        occupancy keeps ordering each bin by ``self.agent_order`` after later
+        moves (refresh_bins), so every result is unchanged -- the exchange adds
+        a bin's agents in the reference's agent order, and agents do not
         interact otherwise.  ``self.agent_order[k]`` is the index (in the
         layout before the first sort) of the agent now stored in column k.
-        Re-sort after agents move.  Colonies whose agent order is itself a
-        result -- division appends daughters in mother order, a row band's
-        router keeps the single-rank order -- keep their layout."""
+        Sort again after agents move to keep the streams.  Colonies whose agent
+        order is itself a result -- division appends daughters in mother order,
+        a row band's router keeps the single-rank order -- keep their layout."""
         if self.lattice is None:
             raise ValueError('sort_by_bin: a lattice colony')
         if self.cells is not None or self.router is not None:
             raise ValueError('sort_by_bin: division and routed bands keep the reference agent order')
         n = self.n
-        perm = torch.sort(self.bin_lin[:n].to(torch.int64), stable=True).indices
+        prev = getattr(self, 'agent_order', None)
+        key = prev if prev is not None else torch.arange(n, dtype=torch.int64, device=self.device)
+        by_key = torch.sort(key[:n], stable=True).indices
+        perm = by_key[torch.sort(self.bin_lin[:n].to(torch.int64)[by_key], stable=True).indices]
         for name in self.agent_array_names() + ['bin_lin', 'bin_ix']:
             t = getattr(self, name)
             if t.dim() == 1:
                 t[:n] = t[:n][perm]
             else:
                 t[:, :n] = t[:, :n][:, perm]
-        prev = getattr(self, 'agent_order', None)
-        self.agent_order = perm if prev is None else prev[perm]
-        self.occ = occupancy(self.bin_lin, n)
+        self.agent_order = key[perm]
+        self.occ = occupancy(self.bin_lin, n, self.agent_order)
         self._layout += 1            # captured graphs hold the old occupancy buffers
         return self.agent_order
 

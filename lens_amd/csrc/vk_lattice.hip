@@ -75,23 +75,21 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
 }
 
 int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h chunk_rows); 0 = auto
-// 0 = workgroup tile (LDS neighbour exchange), 2/3/4 = wave tile lag-1 prefetching 3/6/9 rows,
-// 6 = variant 3 with streaming stores (the default), 12 = variant 6 with stage 0 reading the
-// prefetch ring (no per-group copies of in-flight rows, no vmcnt(0) per group), 13 = variant 12
-// with branch-free buffer stores (exact vmcnt bookkeeping: PD rows of lookahead), 14 = 13 with
-// PD = 3 (a ring of 6 rows, variant 6's unroll and code size), 15 = variant 6 with zigzag chunks
-// (workgroups down a column tile, odd chunks bottom-up in the tolerance mode: shared halo rows
-// read by both neighbours at about the same time), 16 = variant 6 with 6 rows prefetched
-// in the tolerance mode's 10-deep passes (2 waves per SIMD).
-// Retired after A/B on the GPU:
-// 1 (lag-2 wave tile), 5 (4 waves/SIMD cap, spills), 7 (streaming loads), and the round-2
-// experiments 8-11 (four columns per lane, compact boundary body, split stages, LDS-crossbar
-// neighbours) -- bit-exact, none faster.
-static int g_stencil_kernel = 6;
+// Exact mode: 2 / 3 = wave tile lag-1 prefetching 3 / 6 rows, 6 = variant 3 with
+// streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
+// setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default),
+// 21 / 22 = its A/B alternates (2 / 6 rows prefetched),
+// 6 = the variant-6 FMA form (4 FP64 ops per cell-substep instead of 3).
+// Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
+// 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
+// 7 (streaming loads), 8-11 (four columns per lane, compact boundary body, split
+// stages, LDS-crossbar neighbours), 12-16 (prefetch ring, buffer stores, zigzag
+// chunks, 6-row prefetch at depth 10) -- bit-exact, none faster.
+static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 0 || (variant >= 2 && variant <= 4) || variant == 6 || (variant >= 12 && variant <= 16))
+    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 22))
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
@@ -134,6 +132,17 @@ __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ sr
         dst[base + i] = src[base + i];
 }
 
+// One tolerance-mode 10-deep pass (no base plane): pair-sum passes, or the
+// variant-6 FMA form when that variant is selected
+static void launch_fast10(hipStream_t s, const double *src, double *dst, int nf, int64_t fs, int ny, int lo, int hi,
+                          int in_lo, int in_hi, int top, int bot, double coef, const double *mm) {
+    if (g_stencil_kernel >= 20)
+        vk_launch_ps_alt(g_stencil_kernel, 10, s, src, dst, nullptr, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef,
+                         mm);
+    else
+        vk_launch_wl6nt(10, s, src, dst, nullptr, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm);
+}
+
 extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                           int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
                           int32_t hi_max, int32_t edge_top, int32_t edge_bot, int32_t sub_begin,
@@ -172,9 +181,8 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             const int hi = min(hi_max, row_hi + grow);
             const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
             double *dst = (e == n_sub - 1) ? field : (cur == work0 ? work1 : work0);
-            (g_stencil_kernel == 16 ? vk_launch_wl6nt10p6 : vk_launch_wl6nt)(
-                10, s, cur, dst, nullptr, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
-                coeff_dt, uniform);
+            launch_fast10(s, cur, dst, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
+                          coeff_dt, uniform);
             int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
             if (rc) return rc;
             cur = dst;
@@ -186,9 +194,8 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         // convention gives the state after substep 9): the bench's single-pass timing
         const int grow = last_in_call - 9;
         const int lo = max(lo_min, row_lo - grow), hi = min(hi_max, row_hi + grow);
-        (g_stencil_kernel == 16 ? vk_launch_wl6nt10p6 : vk_launch_wl6nt)(
-            10, s, field, work1, nullptr, n_fields, field_stride, ny, lo, hi, max(lo_min, lo - 10),
-            min(hi_max, hi + 10), top_reflect, bot_reflect, coeff_dt, uniform);
+        launch_fast10(s, field, work1, n_fields, field_stride, ny, lo, hi, max(lo_min, lo - 10),
+                      min(hi_max, hi + 10), top_reflect, bot_reflect, coeff_dt, uniform);
         return vk::launch_check("vk_diffuse kernel (depth 10)");
     }
     int depth = g_stencil_depth | 1;   // odd
@@ -221,27 +228,21 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform, 0);
-        } else if (g_stencil_kernel >= 12 && g_stencil_kernel <= 15 && (k == 7 || k == 9 || k == 11)) {
-            auto launch = g_stencil_kernel == 15   ? vk_launch_wl6z
-                          : g_stencil_kernel == 14 ? vk_launch_wl3b
-                          : g_stencil_kernel == 13 ? vk_launch_wl6b
-                                                   : vk_launch_wl6r;
-            launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
-                   coeff_dt, uniform);
-        } else if ((g_stencil_kernel == 6 || g_stencil_kernel == 16 || g_stencil_mode == 1) &&
+        } else if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11) {
+            // tolerance mode, pair-sum passes (the final pass writes the new field as is)
+            vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi,
+                             top_reflect, bot_reflect, coeff_dt, uniform);
+        } else if ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) &&
                    (k == 7 || k == 9 || k == 11)) {
             vk_launch_wl6nt(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
                             bot_reflect, coeff_dt, uniform);
-        } else if (g_stencil_kernel >= 2) {
-            // the final pass also streams the base plane (3 rows ahead): it keeps the
-            // shallow row prefetch so that it still fits 3 waves per SIMD
-            auto launch = (g_stencil_kernel == 2 || f0) ? vk_launch_wl3
-                                                        : (g_stencil_kernel == 4 ? vk_launch_wl9 : vk_launch_wl6);
+        } else {
+            // other depths (and variants 2 / 3): the plain-store wave tiles; the final pass
+            // also streams the base plane (3 rows ahead), so it keeps the shallow row
+            // prefetch and still fits 3 waves per SIMD
+            auto launch = (g_stencil_kernel == 2 || f0) ? vk_launch_wl3 : vk_launch_wl6;
             launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
                    coeff_dt, uniform);
-        } else {
-            vk_launch_tb(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
-                         bot_reflect, coeff_dt, uniform);
         }
         int rc = vk::launch_check("vk_diffuse kernel");
         if (rc) return rc;

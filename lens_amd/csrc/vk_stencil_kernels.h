@@ -14,127 +14,13 @@
 #include "vk_stencil_launch.h"
 
 // ---------------------------------------------------------------------------
-// Temporally blocked stencil: K substeps per pass over HBM.
-//
-// A workgroup owns a tile of TB_BX columns (TB_BX-2K output columns + K halo
-// columns per side) and a chunk of output rows; it streams its input rows
-// top to bottom once.  Substep s (0-based) is a pipeline stage holding a
-// three-row window (up, centre, newest) per column in VGPRs; at iteration i
-// stage s produces row i-2s-1, and its output becomes stage s+1's newest
-// row in iteration i+1, so all K stages of an iteration are independent and
-// share ONE LDS exchange of centre values (left/right neighbours) and ONE
-// barrier (LDS double-buffered by iteration parity).  HBM traffic per pass:
-// one read of (chunk+2K) rows and one write of chunk rows, instead of K reads
-// and K writes.  The arithmetic per cell and substep is the reference's
+// Temporally blocked stencil: K substeps per pass over HBM.  A tile streams its
+// input rows top to bottom once; substep q is a pipeline stage holding its rows
+// in VGPRs, so a pass reads (chunk + 2K) rows and writes chunk rows instead of K
+// reads and K writes.  The arithmetic per cell and substep is the reference's
 // ((up + left) + (-4*c)) + right) + down, c + coef*lap -- fma(-4, c, s) is
 // bit-identical to s + (-4*c) because -4*c is exact.
 // ---------------------------------------------------------------------------
-
-constexpr int TB_BX = 256;
-
-// One pipeline iteration with static register roles U (loop unrolled by 3, so
-// the three-row windows rotate by renaming instead of v_mov).  For stage q:
-// up = X[U], centre = X[U+1], newest = X[U+2] (mod 3); stage q-1's output is
-// stage q's newest next iteration and lands in X[U] once stage q consumed it.
-template <int K, bool EDGE, int U>
-__device__ __forceinline__ void tb_iter(double (&xch)[2][K][TB_BX], double (&X0)[K], double (&X1)[K],
-                                        double (&X2)[K], double (&pf)[3], const double *__restrict__ s,
-                                        double *d, const double *g, int ny, int i,
-                                        int c0, int c1, int in_lo, int in_hi, int top_reflect, int bot_reflect,
-                                        int c, int cc, bool writer, int tl, int tr, bool left_edge,
-                                        bool right_edge, double coef) {
-    double(&UP)[K] = U == 0 ? X0 : (U == 1 ? X1 : X2);
-    double(&CN)[K] = U == 0 ? X1 : (U == 1 ? X2 : X0);
-    double(&NW)[K] = U == 0 ? X2 : (U == 1 ? X0 : X1);
-    const int tid = threadIdx.x;
-    NW[0] = pf[U];                                                    // row i, loaded 3 iterations ago
-    pf[U] = s[(int64_t)min(max(i + 3, in_lo), in_hi - 1) * ny + cc];  // prefetch row i+3
-    const int r_out = i - 2 * K + 1;
-    const bool do_write = writer && r_out >= c0 && r_out < c1;
-    double base = 0.0;
-    if (g && do_write) base = g[(int64_t)r_out * ny + c];
-    const int p = i & 1;
-#pragma unroll
-    for (int q = 0; q < K; ++q) xch[p][q][tid] = CN[q];
-    __syncthreads();
-#pragma unroll
-    for (int q = K - 1; q >= 0; --q) {
-        const int r = i - 2 * q - 1;
-        const double cen = CN[q];
-        const double up = (EDGE && r == top_reflect) ? cen : UP[q];
-        const double dn = (EDGE && r == bot_reflect) ? cen : NW[q];
-        const double lv = xch[p][q][tl], rv = xch[p][q][tr];
-        const double lf = left_edge ? cen : lv;
-        const double rt = right_edge ? cen : rv;
-        const double lap = ((fma(-4.0, cen, up + lf)) + rt) + dn;
-        const double v = cen + coef * lap;
-        if (q + 1 < K) {
-            UP[q + 1] = v;
-        } else if (do_write) {
-            d[(int64_t)r_out * ny + c] = g ? base + (v - base) : v;
-        }
-    }
-}
-
-// EDGE = the tile touches a reflecting boundary (global edge rows/columns);
-// interior tiles (the vast majority) carry no boundary selects at all.
-template <int K, bool EDGE>
-__device__ __forceinline__ void diffuse_tb_body(double (&xch)[2][K][TB_BX], const double *__restrict__ s,
-                                                double *d, const double *g, int ny,
-                                                int c0, int c1, int in_lo, int in_hi, int top_reflect,
-                                                int bot_reflect, int x0, double coef) {
-    const int tid = threadIdx.x;
-    const int c = x0 - K + tid;
-    const int cc = min(max(c, 0), ny - 1);
-    const bool left_edge = EDGE && (c == 0), right_edge = EDGE && (c == ny - 1);
-    const bool writer = tid >= K && tid < TB_BX - K && c < ny;
-    const int tl = max(tid - 1, 0), tr = min(tid + 1, TB_BX - 1);
-
-    double X0[K], X1[K], X2[K], pf[3];
-#pragma unroll
-    for (int q = 0; q < K; ++q) X0[q] = X1[q] = X2[q] = 0.0;
-    const int i0 = c0 - K, i1 = c1 + 2 * K - 1;
-#pragma unroll
-    for (int u = 0; u < 3; ++u) pf[u] = s[(int64_t)min(max(i0 + u, in_lo), in_hi - 1) * ny + cc];
-#define TB_ARGS xch, X0, X1, X2, pf, s, d, g, ny
-#define TB_REST c0, c1, in_lo, in_hi, top_reflect, bot_reflect, c, cc, writer, tl, tr, left_edge, right_edge, coef
-    int i = i0;
-    for (; i + 3 <= i1; i += 3) {
-        tb_iter<K, EDGE, 0>(TB_ARGS, i, TB_REST);
-        tb_iter<K, EDGE, 1>(TB_ARGS, i + 1, TB_REST);
-        tb_iter<K, EDGE, 2>(TB_ARGS, i + 2, TB_REST);
-    }
-    if (i < i1) tb_iter<K, EDGE, 0>(TB_ARGS, i, TB_REST);
-    if (i + 1 < i1) tb_iter<K, EDGE, 1>(TB_ARGS, i + 1, TB_REST);
-#undef TB_ARGS
-#undef TB_REST
-}
-
-template <int K>
-__global__ __launch_bounds__(TB_BX) void k_diffuse_tb(const double *__restrict__ src, double *dst,
-                                                      const double *f0, int64_t field_stride, int ny,
-                                                      int out_lo, int out_hi, int in_lo, int in_hi,
-                                                      int top_reflect, int bot_reflect, int rows_per_chunk,
-                                                      double coef, const double *__restrict__ uniform) {
-    const int f = blockIdx.z;
-    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;  // uniform plane: zero delta
-    const int c0 = out_lo + blockIdx.y * rows_per_chunk;
-    if (c0 >= out_hi) return;
-    const int c1 = min(c0 + rows_per_chunk, out_hi);
-    const int x0 = blockIdx.x * (TB_BX - 2 * K);
-    __shared__ double xch[2][K][TB_BX];
-    const double *s = src + (int64_t)f * field_stride;
-    double *d = dst + (int64_t)f * field_stride;
-    const double *g = f0 ? f0 + (int64_t)f * field_stride : nullptr;
-    // rows this block touches: [c0-K-1, c1+2K); columns [x0-K-1, x0-K+TB_BX]
-    const bool edge = (x0 - K - 1 <= 0) || (x0 - K + TB_BX >= ny - 1) ||
-                      (top_reflect >= c0 - 3 * K - 2 && top_reflect <= c1 + 2 * K) ||
-                      (bot_reflect >= c0 - 3 * K - 2 && bot_reflect <= c1 + 2 * K);
-    if (edge)
-        diffuse_tb_body<K, true>(xch, s, d, g, ny, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, x0, coef);
-    else
-        diffuse_tb_body<K, false>(xch, s, d, g, ny, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, x0, coef);
-}
 
 // ---------------------------------------------------------------------------
 // Wave tiles: one wavefront = one independent tile of 128 columns (two
@@ -181,17 +67,14 @@ __device__ __forceinline__ void wl_store(double *o, double2 v) {
 struct WtLane {
     int cA;              // this lane's first column (cB = cA + 1)
     int ny;
-    uint32_t voff;       // VK_WL_BUF_STORE: byte offset of column A in its row, out of range (store dropped) if not wA
-    bool rev;            // VK_WL_ZIGZAG: this wave walks its chunk bottom-up (physical row = m - logical row)
-    int m;
     bool wA, wB;         // writes its column A / B
     bool lA, rA, lB, rB; // reflect flags (EDGE tiles only)
 };
 
-// Physical row of logical row x, clamped into the pass's input rows [lo, hi).
+// Row x clamped into the pass's input rows [lo, hi).
 __device__ __forceinline__ int64_t wl_row(const WtLane &L, int x, int lo, int hi) {
-    const int r = L.rev ? L.m - x : x;
-    return (int64_t)min(max(r, lo), hi - 1);
+    (void)L;
+    return (int64_t)min(max(x, lo), hi - 1);
 }
 
 template <bool EDGE>
@@ -213,24 +96,9 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
 // the iteration phase U (period 3): up = S[U], centre = S[U+1], fresh = S[U+2].
 // ---------------------------------------------------------------------------
 
-// VK_WL_RING (variant 12/13): stage 0 reads its three rows straight from the
-// prefetch ring, which then holds PD + 3 rows (up, centre, fresh and PD in
-// flight), and the loop is unrolled by that ring length.  Without it the ring
-// (PD slots) and the stage-0 window (3 slots) rotate with different periods, so
-// the register allocator closes each unrolled group with copies of the
-// in-flight rows -- and a vmcnt(0) before them, which drains every load (and
-// streaming store) once per group of PD rows.
-#ifdef VK_WL_RING
-constexpr int wl_ring(int PD) { return PD + 3; }
-constexpr bool WL_RING = true;
-#else
-constexpr int wl_ring(int PD) { return PD; }
-constexpr bool WL_RING = false;
-#endif
-
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
 template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, bool STEADY, int U>
-__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[wl_ring(PD)], double2 (&gp)[3],
+__device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                         const double *__restrict__ s, double *d,
                                         const double *g, const WtLane &L, int i, int c0, int c1,
                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
@@ -240,21 +108,8 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     double2(&CN)[K] = R == 0 ? S1 : (R == 1 ? S2 : S0);
     double2(&FR)[K] = R == 0 ? S2 : (R == 1 ? S0 : S1);
     const int64_t ny = L.ny;
-#ifdef VK_WL_BUF_STORE
-    // keep each iteration's load, stages and store in program order: with the
-    // stores branch-free, a steady group of PD iterations is one basic block, and
-    // the scheduler would otherwise cluster its PD loads at the end of the block
-    __builtin_amdgcn_sched_barrier(0);
-#endif
-    constexpr int NR = wl_ring(PD);
-    if constexpr (WL_RING) {
-        // row j lives in slot (j - i0) mod NR; U = (i - i0) mod NR.  Row i+PD goes
-        // to the slot of row i-3, whose last use (as stage 0's up row) was iteration i-1
-        pf[(U + PD) % NR] = wt_load<EDGE>(s, wl_row(L, i + PD, in_lo, in_hi) * ny, L);
-    } else {
-        FR[0] = pf[U];                                                                      // row i
-        pf[U] = wt_load<EDGE>(s, wl_row(L, i + PD, in_lo, in_hi) * ny, L);             // row i+PD
-    }
+    FR[0] = pf[U];                                                                      // row i
+    pf[U] = wt_load<EDGE>(s, wl_row(L, i + PD, in_lo, in_hi) * ny, L);             // row i+PD
     const int r_out = i - K;
     const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
     double2 base = make_double2(0.0, 0.0);
@@ -267,10 +122,9 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
         // stage q is useful for rows [c0-(K-1-q), c1+(K-1-q)), i.e. i in [c0-K+2+2q, c1+K)
         if (!STEADY && (i < c0 - K + 2 + 2 * q || i >= c1 + K)) continue;
         const int r = i - 1 - q;
-        const bool ring0 = WL_RING && q == 0;
-        const double2 cen = ring0 ? pf[(U + NR - 1) % NR] : CN[q];
-        const double2 up = (EDGE && r == top_reflect) ? cen : (ring0 ? pf[(U + NR - 2) % NR] : UP[q]);
-        const double2 dn = (EDGE && r == bot_reflect) ? cen : (ring0 ? pf[U % NR] : FR[q]);
+        const double2 cen = CN[q];
+        const double2 up = (EDGE && r == top_reflect) ? cen : UP[q];
+        const double2 dn = (EDGE && r == bot_reflect) ? cen : FR[q];
         double leftA = dpp_from_lane_below(cen.y), rightB = dpp_from_lane_above(cen.x);
         double rightA = cen.y, leftB = cen.x;
         if (EDGE) {
@@ -304,24 +158,9 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
             FR[q + 1] = v;
         } else if (row_ok) {
             if (FINAL && !FAST) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
-            const int64_t r_phys = L.rev ? L.m - r_out : r_out;
-            double *o = d + r_phys * ny + L.cA;
+            double *o = d + (int64_t)r_out * ny + L.cA;
             if (!EDGE) {
-#ifdef VK_WL_BUF_STORE
-                // Branch-free store: lanes that do not write carry an out-of-range
-                // offset and the buffer unit drops their store.  With no exec branch
-                // around the store, the compiler's vmcnt bookkeeping counts every
-                // iteration's store, so a row load is awaited only PD rows after its
-                // issue (a masked store made it wait as if no store were in flight:
-                // about PD/2 rows of lookahead).  aux 2 = nt (streaming store).
-                (void)o;
-                typedef int i4v __attribute__((ext_vector_type(4)));
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    (void *)(d + r_phys * ny), 0, (int)(ny * 8), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, v), rs, (int)L.voff, 0, 2);
-#else
                 if (L.wA) wl_store(o, v);
-#endif
             } else {
                 if (L.wA) o[0] = v.x;
                 if (L.wB) o[1] = v.y;
@@ -332,7 +171,7 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
 
 template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
-                                         double2 (&pf)[wl_ring(PD)], double2 (&gp)[3], const double *__restrict__ s, double *d,
+                                         double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *d,
                                          const double *g, const WtLane &L, int i, int c0, int c1,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
                                          double c4) {
@@ -345,7 +184,7 @@ __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], dou
 
 template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
-                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[wl_ring(PD)], double2 (&gp)[3],
+                                                double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                                 const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
@@ -353,15 +192,9 @@ __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...
     const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
     const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
 #define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4
-    constexpr int NU = wl_ring(PD);                  // iterations per unrolled group
+    constexpr int NU = PD;                           // iterations per unrolled group
     int i = i0;
     for (; i + NU <= i1 && i < s_lo; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, false, Us...>(WL_ARGS);   // fill
-#ifdef VK_WL_BUF_STORE
-    // enter the steady loop with no memory operation in flight, so that the
-    // compiler's wait counts at its header come from the loop's own (branch-free)
-    // iterations and not from the fill phase's conditional stores
-    if (!EDGE) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-#endif
     for (; i + NU - 1 <= s_hi; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, true, Us...>(WL_ARGS);          // steady
     for (; i + NU <= i1; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, false, Us...>(WL_ARGS);               // drain
     // tail: fewer than NU iterations, phases 0.. in order
@@ -376,18 +209,14 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
                                                 double coef, double c4) {
-    constexpr int NR = wl_ring(PD);
-    double2 S0[K], S1[K], S2[K], pf[NR], gp[3];
+    double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
 #pragma unroll
     for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
     const int64_t ny = L.ny;
     const int i0 = c0 - K + 2;
     // stage 0's window before the first iteration: up = row i0-2, centre = row i0-1
-    // (ring: slots NR-2 and NR-1)
-    double2 &w_up = WL_RING ? pf[NR - 2] : S0[0];
-    double2 &w_cn = WL_RING ? pf[NR - 1] : S1[0];
-    w_up = wt_load<EDGE>(s, wl_row(L, i0 - 2, in_lo, in_hi) * ny, L);
-    w_cn = wt_load<EDGE>(s, wl_row(L, i0 - 1, in_lo, in_hi) * ny, L);
+    S0[0] = wt_load<EDGE>(s, wl_row(L, i0 - 2, in_lo, in_hi) * ny, L);
+    S1[0] = wt_load<EDGE>(s, wl_row(L, i0 - 1, in_lo, in_hi) * ny, L);
 #pragma unroll
     for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, wl_row(L, i0 + u, in_lo, in_hi) * ny, L);
 #pragma unroll
@@ -395,7 +224,7 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
         gp[u] = FINAL && !FAST && (L.wA || L.wB)
                     ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
                     : make_double2(0.0, 0.0);
-    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST, SC>(std::make_integer_sequence<int, NR>(), S0, S1, S2, pf, gp, s, d, g, L,
+    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST, SC>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L,
                                               c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
@@ -415,17 +244,8 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int lane = threadIdx.x & 63;
     if (wave >= tiles_x * chunks_y * n_fields) return;
-#ifdef VK_WL_ZIGZAG
-    // the 4 waves of a workgroup take 4 vertically adjacent chunks of one column
-    // tile, odd chunks walked bottom-up: each chunk boundary's halo rows are then
-    // read by both neighbours at about the same time (both at their start or both
-    // at their end), mostly on one CU
-    const int ty = wave % chunks_y;
-    const int tx = (wave / chunks_y) % tiles_x;
-#else
     const int tx = wave % tiles_x;
     const int ty = (wave / tiles_x) % chunks_y;
-#endif
     const int f = wave / (tiles_x * chunks_y);
     if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;
     const int c0 = out_lo + ty * rows_per_chunk;
@@ -433,13 +253,10 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     const int x0 = tx * W;
     WtLane L;
     L.ny = ny;
-    L.rev = false;
-    L.m = 0;
     L.cA = x0 - KH + 2 * lane;
     const int cB = L.cA + 1;
     L.wA = lane >= KH / 2 && lane < 64 - KH / 2 && L.cA < ny;
     L.wB = lane >= KH / 2 && lane < 64 - KH / 2 && cB < ny;
-    L.voff = L.wA ? (uint32_t)L.cA * 8u : 0x80000000u;
     L.lA = L.cA == 0;
     L.rA = L.cA == ny - 1;
     L.lB = cB == 0;
@@ -451,12 +268,6 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
                       (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
                       (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
     const double c4 = 1.0 - 4.0 * coef;      // FAST only
-#ifdef VK_WL_ZIGZAG
-    // only the tolerance mode: (N + S) + (E + W) is symmetric in N and S, so a
-    // bottom-up walk gives the same bits (the exact mode's order is not)
-    L.rev = FAST && !edge && (ty & 1);
-    L.m = c0 + c1 - 1;
-#endif
     if constexpr (FAST) {
         // the scaled form while c4^-K stays far from overflow (|c4| >= 1e-3, i.e.
         // coef not within 2.5e-4 of 1/4; coef = 0 gives the identity exactly)

@@ -15,11 +15,7 @@ extern int g_stencil_mode;   // 0 = bit-exact (default), 1 = tolerance / FMA (vk
 
 void vk_launch_wl3(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 3 rows prefetched
 void vk_launch_wl6(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 6 rows prefetched
-void vk_launch_wl9(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 9 rows prefetched
-void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS);        // as wl6 with streaming stores (k = 7, 9, 11)
-void vk_launch_wl6r(VK_STENCIL_LAUNCH_ARGS);         // wl6nt, stage 0 on the prefetch ring (k = 7, 9, 11)
-void vk_launch_wl6b(VK_STENCIL_LAUNCH_ARGS);         // wl6r with branch-free buffer stores (k = 7, 9, 11)
-void vk_launch_wl3b(VK_STENCIL_LAUNCH_ARGS);         // wl6b with 3 rows of lookahead (k = 7, 9, 11)
-void vk_launch_wl6z(VK_STENCIL_LAUNCH_ARGS);
-void vk_launch_wl6nt10p6(VK_STENCIL_LAUNCH_ARGS);   // 10-deep fma pass, 6 rows prefetched (variant 16)         // wl6nt with zigzag chunks (k = 7, 9, 11)
-void vk_launch_tb(VK_STENCIL_LAUNCH_ARGS);           // workgroup tile, LDS neighbour exchange
+void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS);        // as wl6 with streaming stores (k = 7, 9, 11; 10 tolerance mode)
+void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS);           // tolerance mode, pair-sum form (k = 3, 5, 7, 9, 11)
+void vk_launch_ps10(VK_STENCIL_LAUNCH_ARGS);         // the same, k = 10
+void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS);   // variant 20-22 dispatch (21 / 22: A/B alternates)

@@ -22,9 +22,3 @@ void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS) {
     else if (k == 10)   // tolerance mode only; 3 rows prefetched keep it at 154 VGPRs (3 waves per SIMD)
         vk_nt::launch_fast<10, 3>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
 }
-
-// variant 16: the 10-deep tolerance-mode pass with 6 rows prefetched (170 VGPRs, 2 waves per SIMD)
-void vk_launch_wl6nt10p6(VK_STENCIL_LAUNCH_ARGS) {
-    (void)k;
-    vk_nt::launch_fast<10, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
-}

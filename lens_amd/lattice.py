@@ -304,10 +304,16 @@ class Lattice:
             'vk_exchange_atomic')
 
 
-def occupancy(bin_lin: torch.Tensor, n_agents: int):
-    """Bin -> agents CSR in agent order (stable sort), for :meth:`Lattice.exchange_sorted`."""
+def occupancy(bin_lin: torch.Tensor, n_agents: int, order_key: Optional[torch.Tensor] = None):
+    """Bin -> agents CSR for :meth:`Lattice.exchange_sorted`: each bin's agents in
+    agent order -- their column order, or ascending ``order_key`` (the agents'
+    reference order when the columns were permuted, Colony.sort_by_bin)."""
     b = bin_lin[:n_agents].to(torch.int64)
-    order = torch.sort(b, stable=True).indices
+    if order_key is None:
+        order = torch.sort(b, stable=True).indices
+    else:
+        by_key = torch.sort(order_key[:n_agents].to(torch.int64), stable=True).indices
+        order = by_key[torch.sort(b[by_key], stable=True).indices]
     sb = b[order]
     if n_agents == 0:
         z = torch.zeros(0, dtype=torch.int32, device=bin_lin.device)

@@ -374,10 +374,8 @@ def test_dopri5_wave_equals_lane_variant_small_network(dev):
     assert np.mean(out[0][1] == out[1][1]) > 0.99
 
 
-@pytest.mark.parametrize('variant,depth', [(0, 1), (0, 3), (0, 15), (2, 3), (2, 5), (2, 9), (2, 13), (2, 15),
-                                           (3, 7), (3, 9), (4, 5), (4, 11), (6, 5), (6, 7), (6, 9), (6, 11),
-                                           (12, 7), (12, 9), (12, 11), (13, 5), (13, 7), (13, 9), (13, 11),
-                                           (14, 7), (14, 9), (14, 11), (15, 7), (15, 9), (15, 11)])
+@pytest.mark.parametrize('variant,depth', [(2, 1), (2, 3), (2, 5), (2, 9), (2, 13), (2, 15), (3, 7), (3, 9),
+                                           (3, 11), (6, 5), (6, 7), (6, 9), (6, 11), (6, 15), (20, 9), (20, 3)])
 def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
     """Every kernel variant and temporal-blocking depth reproduces
     scipy.ndimage.convolve bit for bit."""
@@ -401,12 +399,9 @@ def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
         stencil_kernel(prev_k, 0)
 
 
-@pytest.mark.parametrize('variant,depth,rows', [(0, 15, 64), (2, 9, 64), (2, 7, 128), (2, 11, 32), (2, 15, 256),
-                                                (3, 9, 64), (3, 13, 48), (4, 9, 96), (4, 7, 40), (6, 9, 64),
-                                                (6, 11, 48), (6, 7, 40), (6, 9, 17), (12, 9, 64), (12, 11, 48),
-                                                (12, 7, 40), (12, 9, 17), (13, 9, 64), (13, 11, 48), (13, 7, 40),
-                                                (13, 9, 17), (13, 9, 8), (14, 9, 64), (14, 11, 48), (14, 7, 40),
-                                                (14, 9, 17), (15, 9, 64), (15, 11, 48), (15, 7, 40), (15, 9, 17)])
+@pytest.mark.parametrize('variant,depth,rows', [(2, 9, 64), (2, 7, 128), (2, 11, 32), (2, 15, 256), (3, 9, 64),
+                                                (3, 13, 48), (6, 9, 64), (6, 11, 48), (6, 7, 40), (6, 9, 17),
+                                                (6, 9, 8), (20, 9, 34)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
 def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
     """Multi-tile / multi-chunk geometry: interior tiles, ragged last tile and
