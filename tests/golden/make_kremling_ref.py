@@ -25,7 +25,13 @@ switch on internal G6P (> 0.01: G6P uptake; else lactose):
   tolerances, i.e. the reference's literal call.
 
 No reference source is copied into the repository: the file is parsed at
-generation time only.
+generation time only.  The reference is untrusted input, so nothing of it runs
+before an AST whitelist has passed it (``_check_params`` / ``_check_model``):
+the parameters may only be a dict of numeric constants and arithmetic on them;
+the model only arithmetic, comparisons, subscripts, assignments, ``if`` and
+``return``, calls to ``np.zeros_like`` and ``state_keys.index``, and names that
+are its own locals, its argument, ``p``, ``state_keys`` or ``np``.  Both are
+then evaluated with an empty ``__builtins__``.
 
     python tests/golden/make_kremling_ref.py
 """
@@ -43,11 +49,54 @@ REF = '/root/reference/vivarium/processes/Kremling2007_transport.py'
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'kremling_ref.npz')
 
 
+_ARITH = (ast.Add, ast.Sub, ast.Mult, ast.Div, ast.Pow, ast.USub, ast.UAdd)
+_CALLS = {('np', 'zeros_like'), ('state_keys', 'index')}
+
+
+def _check_params(expr):
+    """DEFAULT_PARAMETERS: a dict literal of string keys and numeric constants,
+    with arithmetic on constants allowed (e.g. 2.4 * 60)."""
+    for n in ast.walk(expr):
+        ok = isinstance(n, (ast.Dict, ast.Constant, ast.BinOp, ast.UnaryOp, ast.Load) + _ARITH)
+        if isinstance(n, ast.Constant) and not isinstance(n.value, (int, float, str)):
+            ok = False
+        if not ok:
+            raise ValueError('DEFAULT_PARAMETERS: disallowed node %s' % ast.dump(n)[:80])
+
+
+def _check_model(fn):
+    """model(state, t): arithmetic over names, subscripts and the two calls in
+    _CALLS; every name is an argument, a local it assigns, or p / state_keys / np."""
+    args = {a.arg for a in fn.args.args}
+    local = {t.id for n in ast.walk(fn) if isinstance(n, ast.Assign) for t in n.targets if isinstance(t, ast.Name)}
+    names = args | local | {'p', 'state_keys', 'np'}
+    allowed = (ast.FunctionDef, ast.arguments, ast.arg, ast.Assign, ast.Return, ast.If, ast.Expr, ast.Compare,
+               ast.BinOp, ast.UnaryOp, ast.Name, ast.Load, ast.Store, ast.Constant, ast.Subscript, ast.Call,
+               ast.Attribute, ast.Gt, ast.Lt, ast.GtE, ast.LtE) + _ARITH
+    for n in ast.walk(fn):
+        if not isinstance(n, allowed):
+            raise ValueError('model: disallowed node %s' % type(n).__name__)
+        if isinstance(n, ast.Name) and n.id not in names:
+            raise ValueError('model: unknown name %s' % n.id)
+        if isinstance(n, ast.Attribute):
+            if not (isinstance(n.value, ast.Name) and (n.value.id, n.attr) in _CALLS):
+                raise ValueError('model: disallowed attribute %s' % ast.unparse(n))
+        if isinstance(n, ast.Call):
+            if not (isinstance(n.func, ast.Attribute) and isinstance(n.func.value, ast.Name) and
+                    (n.func.value.id, n.func.attr) in _CALLS) or n.keywords:
+                raise ValueError('model: disallowed call %s' % ast.unparse(n))
+        if isinstance(n, ast.Constant) and not isinstance(n.value, (int, float, str)):
+            raise ValueError('model: disallowed constant %r' % (n.value,))
+        if isinstance(n, ast.Expr) and not isinstance(n.value, ast.Constant):   # docstrings only
+            raise ValueError('model: disallowed statement %s' % ast.unparse(n))
+
+
 def _pieces(path):
     tree = ast.parse(open(path).read(), path)
     params = keys = model = None
     for node in tree.body:
         if isinstance(node, ast.Assign) and any(getattr(t, 'id', None) == 'DEFAULT_PARAMETERS' for t in node.targets):
+            _check_params(node.value)
             params = eval(compile(ast.Expression(node.value), path, 'eval'), {'__builtins__': {}})
         if isinstance(node, ast.ClassDef) and node.name == 'Transport':
             nu = next(f for f in node.body if isinstance(f, ast.FunctionDef) and f.name == 'next_update')
@@ -56,8 +105,9 @@ def _pieces(path):
                 if isinstance(st, ast.Assign) and getattr(st.targets[0], 'id', None) == 'combined_state':
                     keys = [k.value for k in st.value.keys]
     assert params and keys and model, 'reference layout changed'
+    _check_model(model)
     mod = ast.Module(body=[model], type_ignores=[])
-    ns = {'np': np, 'p': dict(params), 'state_keys': list(keys)}
+    ns = {'__builtins__': {}, 'np': np, 'p': dict(params), 'state_keys': list(keys)}
     exec(compile(mod, path, 'exec'), ns)
     return ns['model'], params, keys
 
