@@ -599,14 +599,46 @@ def main():
     elif lat is None:
         kin_ms = sum(t['kin'][0].elapsed_time(t['kin'][1]) for t in timing) / args.steps
         diff_ms = None
+    elif use_graph and not banded:
+        # The kinetics / diffusion split from graph-replayed steps: a replay of the
+        # timed steps' graph with device timestamps (vk_timestamp, one-lane kernels)
+        # before the kinetics, after it, and at the end of every step.  Each stamp
+        # adds a launch boundary (~1-2 us) inside the step; the stamped step is
+        # reported beside ms_per_step.  (torch refuses events inside a graph on
+        # ROCm; eager steps after the timed region ran ~7 % longer than replayed
+        # ones, r03 VERDICT.)
+        from lens_amd import native
+        stamps = torch.zeros(3 * per_graph, dtype=torch.int64, device=dev)
+        replay_s = col.capture(1.0, per_graph, stamps=stamps)
+        replay_s()                        # upload
+        barrier()
+        kin_l, diff_l, step_l, gap_l = [], [], [], []
+        khz = float(native._lib.vk_wall_clock_khz())
+        for _ in range(3):
+            replay_s()
+            barrier()
+            s_ = stamps.cpu().numpy().reshape(per_graph, 3).astype(np.float64) / khz      # ms
+            kin_l += list(s_[:, 1] - s_[:, 0])
+            diff_l += list(s_[:, 2] - s_[:, 1])
+            step_l += list(np.diff(s_[:, 0]))
+            gap_l += list(s_[1:, 0] - s_[:-1, 2])          # two adjacent stamps, nothing between
+        # each segment spans one stamp-to-stamp launch boundary more than its kernels:
+        # the interval between two adjacent stamps (end of step k -> start of step k+1)
+        gap = float(np.median(gap_l)) if gap_l else 0.0
+        kin_ms, diff_ms = float(np.median(kin_l)) - gap, float(np.median(diff_l)) - gap
+        graph_info['kernel_split_from'] = (
+            'median over %d graph-replayed steps with device timestamps before the kinetics, after it and at the '
+            'end of each step (vk_timestamp, %g kHz clock), less the stamp-to-stamp interval of two adjacent '
+            'stamps (%.4f ms); the stamped step (three stamps) %.4f ms' % (3 * per_graph, khz, gap,
+                                                                            float(np.median(step_l))))
+        graph_info['stamped_step_ms'] = float(np.median(step_l)) if step_l else None
+        graph_info['stamp_gap_ms'] = gap
     else:
-        # The kinetics / diffusion split: eager steps after the timed region with
-        # HIP events around the kinetics launch and the diffusion passes.  A
-        # lattice step is ~10x longer on the GPU than its issue from Python, so
-        # from the second step on the host runs ahead and the events bracket
-        # kernel time only (the first step still waits for its issue: dropped).
-        # (Segment graphs timed between replays add each graph launch's GPU-side
-        # gap, ~10 us, and torch refuses events inside a graph on ROCm.)
+        # Eager multi-GPU / dividing steps: HIP events around the kinetics launch and
+        # the diffusion passes of eager steps after the timed region.  A lattice step
+        # is ~10x longer on the GPU than its issue from Python, so from the second
+        # step on the host runs ahead and the events bracket kernel time only (the
+        # first step still waits for its issue: dropped).
         marks = [mk() for _ in range(SPLIT_STEPS)]
         barrier()
         for t_k in marks:

@@ -201,19 +201,24 @@ int vk_diffuse_delta(double *field, double *work0, double *work1, double *delta,
                      vk_stream_t stream);
 
 /* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
- * 1..15; 1 = one launch per substep; default 9).  Each call is planned as the
- * fewest odd-depth passes <= k, as even as possible.  Returns the previous
- * value; k outside 1..15 only queries.  Bit-identical for every depth.     */
+ * 1..15; 1 = one launch per substep; default 9; or 10: a tolerance-mode whole
+ * step of a multiple of 10 substeps as 10-deep passes over three buffers).
+ * Each call is planned as the fewest odd-depth passes <= k, as even as
+ * possible.  Returns the previous value; other k only query.  Exact mode:
+ * bit-identical for every depth.                                           */
 int vk_set_stencil_depth(int32_t k);
 
-/* Fused-pass kernel variant: 0 = workgroup tile with an LDS neighbour
- * exchange; 2 / 3 / 4 = wave tile with DPP lane shifts, stage q lagging q
- * rows (two live rows per stage), 3 / 6 / 9 rows prefetched; 6 = variant 3
- * with streaming (non-temporal) stores (default).  Other values are ignored
- * (retired variants 1, 5, 7-11).  rows = output rows per tile
- * (8..4096; 0 = auto from the band height; other values keep the current).
- * Returns the previous variant.  Tuning only: results are bit-identical for
- * every setting.                                                           */
+/* Fused-pass kernel variant.  Exact mode: 2 / 3 = wave tile with DPP lane
+ * shifts, stage q lagging q rows (two live rows per stage), 3 / 6 rows
+ * prefetched; 6 = variant 3 with streaming (non-temporal) stores (the exact
+ * mode's kernel for 6 and 20-22).  Tolerance mode: 20 = pair-sum passes,
+ * (W+N)+(S+E) with each pair added once and used by two cells, 3 FP64 ops
+ * per cell-substep (default); 21 / 22 = 20 with 2 / 6 rows prefetched; 6 =
+ * the 4-op FMA form.  Other values are ignored (retired variants 0, 1, 4, 5,
+ * 7-16).  rows = output rows per tile (8..4096; 0 = auto from
+ * the band height; other values keep the current).  Returns the previous
+ * variant.  Tuning only: exact-mode results are bit-identical for every
+ * setting; tolerance-mode results stay within 1e-13 of them.               */
 int vk_set_stencil_kernel(int32_t variant, int32_t rows);
 
 /* Arithmetic mode of vk_diffuse's fused passes.  0 (default) = bit-identical
@@ -227,6 +232,16 @@ int vk_set_stencil_kernel(int32_t variant, int32_t rows);
  * vk_diffuse_delta stay exact.  Returns the previous mode; other values only
  * query.                                                                   */
 int vk_set_stencil_mode(int32_t mode);
+
+/* out[idx] = the device's constant-rate wall clock (s_memrealtime ticks, see
+ * vk_wall_clock_khz), written by one lane of a one-wave launch on `stream`.
+ * Not a reference interface: the bench stamps segment boundaries inside a
+ * replayed HIP graph with it (torch refuses events in graphs on ROCm).     */
+int vk_timestamp(uint64_t *out, int32_t idx, vk_stream_t stream);
+
+/* Tick rate of vk_timestamp's clock in kHz (hipDeviceAttributeWallClockRate
+ * of the current device); 0 on error.                                       */
+int64_t vk_wall_clock_khz(void);
 
 /* dst[map_row[i]*ld + a] = fields[map_field[i]*field_stride + bin_lin[a]]. */
 int vk_gather(const double *fields, int64_t field_stride, const int32_t *bin_lin,

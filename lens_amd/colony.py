@@ -267,10 +267,15 @@ class Colony:
             if getattr(self, 'attempts', None) is not None:
                 self.attempts += self.nsteps[:self.n].sum()
 
-    def step(self, dt: float = 1.0, halo_exchange=None, allreduce=None, timing=None):
+    def step(self, dt: float = 1.0, halo_exchange=None, allreduce=None, timing=None, stamp=None):
         """One timestep.  ``timing`` (optional) = {'kin': (ev0, ev1), 'diff': (ev0, ev1)}
-        of torch.cuda.Events recorded on the launch stream around those kernels."""
+        of torch.cuda.Events recorded on the launch stream around those kernels.
+        ``stamp`` (optional, a callable of 0 / 1 / 2) writes a device timestamp
+        on the launch stream before the kinetics, after it, and at the end of
+        the step (bench instrumentation that also works inside a captured graph)."""
         timing = {k: v for k, v in (timing or {}).items() if v is not None}
+        if stamp is not None:
+            stamp(0)
         if self.lattice is not None and self.overlap_kinetics:
             # kinetics + gather read only the pre-step field and agent state, so
             # they run on a side stream beside the diffusion passes; the pass
@@ -302,6 +307,8 @@ class Colony:
         self.kinetics(dt)
         if 'kin' in timing:
             timing['kin'][1].record()
+        if stamp is not None:
+            stamp(1)
         if self.lattice is not None:
             lat = self.lattice
             self.gather_external()                       # pre-step field (one-step lag)
@@ -319,6 +326,8 @@ class Colony:
                     self.env_binvol_avogadro, native.stream_handle()), 'vk_exchange_atomic')
             self._env_to_external()
         self._finish_step(dt)
+        if stamp is not None:
+            stamp(2)
 
     # -- multi-rate advance (Experiment.update, experiment.py:1351-1450) -------------
     def run(self, interval: float, kinetics_dt: float = 1.0, diffusion_dt: float = 1.0, halo_exchange=None,
@@ -414,7 +423,7 @@ class Colony:
                 lat.exchange_atomic(self.bin_lin, self.n, self.counts, self.map_exch_count,
                                     self.map_exch_field)
 
-    def capture(self, dt: float = 1.0, steps: int = 1):
+    def capture(self, dt: float = 1.0, steps: int = 1, stamps=None):
         """Capture ``steps`` timesteps into one HIP graph (torch.cuda.CUDAGraph)
         and return a function that replays them.
 
@@ -430,7 +439,10 @@ class Colony:
         so the colony state is unchanged until the first replay. The graph
         holds the buffers and the agent count of capture time: set_agents()
         values may change between replays (they are copied in place), but a
-        re-binning of moved agents invalidates it (replay raises)."""
+        re-binning of moved agents invalidates it (replay raises).
+        ``stamps`` (optional, a device int64 tensor of 3 * steps) records each
+        replayed step's segment boundaries (:meth:`step`'s ``stamp``) at
+        [3k, 3k + 1, 3k + 2] -- vk_timestamp ticks, vk_wall_clock_khz per ms."""
         lat = self.lattice
         if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
                 (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
@@ -443,8 +455,12 @@ class Colony:
         t0, s0 = self.time, self.step_index
         layout, n = self._layout, self.n
         with torch.cuda.graph(graph):
-            for _ in range(steps):
-                self.step(dt)
+            for k in range(steps):
+                stamp = None
+                if stamps is not None:
+                    stamp = (lambda tag, k=k: native.check(native._lib.vk_timestamp(
+                        native.ptr(stamps), 3 * k + tag, native.stream_handle()), 'vk_timestamp'))
+                self.step(dt, stamp=stamp)
         self.time, self.step_index = t0, s0      # capture ran nothing
 
         def replay():
@@ -457,6 +473,7 @@ class Colony:
             self.step_index += steps
 
         replay.graph = graph      # keep the graph (and its memory pool) alive with the replayer
+        replay.stamps = stamps
         return replay
 
     def capture_banded(self, dt: float = 1.0, halo_exchange=None, allreduce=None):

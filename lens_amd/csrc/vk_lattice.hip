@@ -121,6 +121,30 @@ extern "C" int vk_set_stencil_depth(int32_t k) {
     return prev;
 }
 
+// ---------------------------------------------------------------------------
+// Segment timestamps (bench instrumentation inside a replayed HIP graph)
+// ---------------------------------------------------------------------------
+
+__global__ void k_timestamp(uint64_t *out, int idx) {
+    if (threadIdx.x == 0) out[idx] = wall_clock64();
+}
+
+extern "C" int vk_timestamp(uint64_t *out, int32_t idx, vk_stream_t stream) {
+    if (!out || idx < 0) {
+        vk::set_error("vk_timestamp: bad arguments");
+        return VK_ERR_ARG;
+    }
+    hipLaunchKernelGGL(k_timestamp, dim3(1), dim3(64), 0, (hipStream_t)stream, out, idx);
+    return vk::launch_check("k_timestamp");
+}
+
+extern "C" int64_t vk_wall_clock_khz(void) {
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess) return 0;
+    return khz;
+}
+
 // rows [lo, hi) of every non-uniform plane: dst <- src
 __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ src, double *dst,
                                                    int64_t field_stride, int64_t off, int64_t count,

@@ -1,0 +1,161 @@
+"""Division for the Process-API loop (:class:`lens_amd.engine.Experiment`).
+
+Restates what a dividing compartment needs from the reference:
+
+* the divider registry (vivarium/core/registry.py:197-280): ``set``,
+  ``split`` (ints: the odd count goes to a random daughter via
+  ``random.choice``; ``inf``/``'Infinity'`` kept; floats halved), ``zero``,
+  ``split_dict``, ``no_divide``; a schema ``_divider`` may also be a callable
+  or ``{'divider': fn, 'topology': {...}}`` (the divider gets the states at
+  those paths, relative to the store holding the leaf);
+* ``MetaDivision`` (vivarium/processes/meta_division.py:24-88), the deriver
+  that turns ``global.divide`` into a ``_divide`` update with the daughters'
+  generated processes and topology, ids from ``daughter_phylogeny_id``;
+* ``GrowthProtein`` (vivarium/processes/growth_protein.py:20-107), the
+  ``growth_division_minimal`` growth process (units removed: masses in fg,
+  protein as a count).
+
+The store side (``_divide`` / ``_generate`` / ``_delete`` / ``_add`` in
+``Store.apply_update``, experiment.py:628-697) lives in
+:meth:`lens_amd.engine.Experiment._structural`.  The device-resident colony
+(:class:`lens_amd.colony.Colony`) divides on the GPU instead (vk_divide_*).
+"""
+
+from __future__ import annotations
+
+import random
+
+import numpy as np
+
+from lens_amd.process import ProcessBase
+
+# derive_globals.py:16 takes scipy.constants.N_A; the reference fixtures were made
+# with scipy < 1.4, i.e. the CODATA-2014 value (SURVEY.md §0 finding 2)
+AVOGADRO = 6.022140857e23
+
+
+def divide_set(state):
+    return [state, state]
+
+
+def divide_split(state):
+    """registry.py:205-236."""
+    if isinstance(state, (int, np.integer)) and not isinstance(state, bool):
+        remainder = state % 2
+        half = int(state / 2)
+        if random.choice([True, False]):
+            return [half + remainder, half]
+        return [half, half + remainder]
+    if state == float('inf') or state == 'Infinity':
+        return [state, state]
+    if isinstance(state, (float, np.floating)):
+        half = state / 2
+        return [half, half]
+    raise Exception('can not divide state {} of type {}'.format(state, type(state)))
+
+
+def divide_zero(state):
+    return [0, 0]
+
+
+def divide_split_dict(state):
+    """registry.py:246-272: the first half of the keys to one daughter, the rest to the other."""
+    if state is None:
+        state = {}
+    d1 = dict(list(state.items())[len(state) // 2:])
+    d2 = dict(list(state.items())[:len(state) // 2])
+    return [d1, d2]
+
+
+def assert_no_divide(state):
+    raise AssertionError('division cannot occur during this process')
+
+
+DIVIDERS = {'set': divide_set, 'split': divide_split, 'split_dict': divide_split_dict, 'zero': divide_zero,
+            'no_divide': assert_no_divide}
+
+
+def daughter_phylogeny_id(mother_id):
+    """meta_division.py:15-18."""
+    return [str(mother_id) + '0', str(mother_id) + '1']
+
+
+def divider_set_false(state):
+    return [False, False]
+
+
+class MetaDivision(ProcessBase):
+    """meta_division.py:24-88: a deriver; when ``global.divide`` is set it
+    returns ``{'cells': {'_divide': {'mother': agent_id, 'daughters': [...]}}}``
+    with each daughter's processes and topology from ``compartment`` (an object
+    with ``generate(config) -> {'processes', 'topology'}``, or a callable of
+    the config)."""
+
+    name = 'meta_division'
+    defaults = {'initial_state': {}, 'daughter_path': ('cell',), 'daughter_ids_function': daughter_phylogeny_id}
+
+    def __init__(self, initial_parameters=None):
+        initial_parameters = dict(initial_parameters or {})
+        self.division = 0
+        self.agent_id = initial_parameters['agent_id']
+        self.compartment = initial_parameters['compartment']
+        self.daughter_ids_function = initial_parameters.get('daughter_ids_function',
+                                                            self.defaults['daughter_ids_function'])
+        self.daughter_path = tuple(initial_parameters.get('daughter_path', self.defaults['daughter_path']))
+        params = {k: v for k, v in initial_parameters.items() if k not in ('compartment', 'daughter_ids_function')}
+        super().__init__(params)
+
+    def is_deriver(self):
+        return True
+
+    def ports_schema(self):
+        return {'global': {'divide': {'_default': False, '_updater': 'set', '_divider': divider_set_false}},
+                'cells': {'*': {}}}
+
+    def _generate(self, config):
+        gen = getattr(self.compartment, 'generate', None)
+        return gen(config) if gen is not None else self.compartment(config)
+
+    def next_update(self, timestep, states):
+        if not states['global']['divide']:
+            return {}
+        daughters = []
+        for daughter_id in self.daughter_ids_function(self.agent_id):
+            compartment = self._generate({'agent_id': daughter_id})
+            daughters.append({'daughter': daughter_id, 'path': (daughter_id,) + self.daughter_path,
+                              'processes': compartment['processes'], 'topology': compartment['topology'],
+                              'initial_state': {}})
+        return {'cells': {'_divide': {'mother': self.agent_id, 'daughters': daughters}}}
+
+
+class GrowthProtein(ProcessBase):
+    """growth_protein.py:20-107 with units removed: the protein count grows by
+    exp(rate * dt), the fractional remainder drawn with np.random.random(); the
+    cell divides once the count reaches twice the initial protein."""
+
+    name = 'growth_protein'
+    defaults = {'initial_mass': 1339.0, 'protein_mw': 2.09e4, 'growth_rate': 0.000275,
+                'global_deriver_key': 'global_deriver', 'mass_deriver_key': 'mass_deriver'}
+
+    def __init__(self, initial_parameters=None):
+        super().__init__(initial_parameters)
+        p = self.parameters
+        self.growth_rate = p['growth_rate']
+        # (initial_mass fg).to('g') / (protein_mw g/mol) * N_A
+        self.initial_protein = p['initial_mass'] * 1e-15 / p['protein_mw'] * AVOGADRO
+        self.divide_protein = self.initial_protein * 2
+
+    def ports_schema(self):
+        return {'internal': {'protein': {'_default': self.initial_protein, '_divider': 'split', '_emit': True}},
+                'global': {'volume': {'_updater': 'set', '_divider': 'split'},
+                           'divide': {'_default': False, '_updater': 'set'}}}
+
+    def next_update(self, timestep, states):
+        protein = states['internal']['protein']
+        total_protein = protein * np.exp(self.parameters['growth_rate'] * timestep)
+        new_protein = int(total_protein - protein)
+        extra = total_protein - int(total_protein)
+        if np.random.random() < extra:
+            new_protein += 1
+        return {'internal': {'protein': new_protein}, 'global': {'divide': bool(protein >= self.divide_protein)}}
+

@@ -15,7 +15,15 @@
   leaves apply the schema updater (accumulate by default) or an inline
   ``{'_value', '_updater'}`` one; ``update_field_with_exchange`` gets the
   agent's ``global`` / ``dimensions`` states through its port_mapping
-  (registry.py:149-183).
+  (registry.py:149-183);
+* structural updates at a branch, in the reference's order (:628-697):
+  ``_delete`` (paths), ``_add`` (path + state), ``_generate`` (path,
+  processes, topology, initial_state: the processes join the tree and their
+  ports' schemas register) and ``_divide`` (the mother's values are copied,
+  each leaf's ``_divider`` splits them -- :mod:`lens_amd.division` -- the
+  daughters are generated at the end of the branch in order, then the mother
+  is deleted); the process tree is walked again after any of them, and a
+  deriver deleted earlier in the same pass does not run (:1321-1327).
 
 What is batched (SURVEY.md §8 a9 + N2):
 
@@ -40,6 +48,8 @@ from typing import Dict, List, Tuple
 
 import numpy as np
 
+from lens_amd.division import DIVIDERS
+from lens_amd.process import deep_merge
 from lens_amd.registry import DeviceField, make_update_field_with_exchange
 
 INFINITY = float('inf')
@@ -96,6 +106,10 @@ class Experiment:
         self._port_nodes: Dict[Tuple, Tuple] = {}
         self._plans: Dict[Tuple, Tuple] = {}        # process path -> (version, process, kinetics plan)
         self._version = 0
+        self.dividers: Dict[Tuple, object] = {}   # store path (with '*' globs) -> schema _divider
+        self._div_globs: List[Tuple] = []
+        self._structure = 0                        # moves when processes join or leave the tree
+        self._deleted = set()                      # ids of processes deleted from the tree
         self._state_seen = None
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
@@ -139,17 +153,26 @@ class Experiment:
         self._updater_cache.clear()
         self._leaf_updaters.clear()
         keys = [k for k in schema if not k.startswith('_')]
-        if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
+        if ('_default' in schema or '_value' in schema or '_updater' in schema or '_divider' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
                 self.schema.setdefault(path, schema['_updater'])
                 if '*' in path and path not in self._globs:
                     self._globs.append(path)
-            if '*' not in path:
+            if '_divider' in schema:
+                self.dividers.setdefault(path, schema['_divider'])
+                if '*' in path and path not in self._div_globs:
+                    self._div_globs.append(path)
+            if '*' not in path and ('_default' in schema or '_value' in schema):
                 node = self.state
                 for key in path[:-1]:
                     node = node.setdefault(key, {})
                 if path[-1] not in node:
                     node[path[-1]] = schema.get('_value', schema.get('_default'))
+            elif '*' not in path:
+                node = self.state
+                for key in path[:-1]:
+                    node = node.setdefault(key, {})
+                node.setdefault(path[-1], None)    # a store without a default holds None (Store.apply_defaults)
             return
         for k in keys:
             self._register(path + (k,), schema[k])
@@ -207,6 +230,10 @@ class Experiment:
         inline = isinstance(update, dict) and '_updater' in update
         if isinstance(current, dict) and not inline:
             cpath = ppath + (key,)
+            if isinstance(update, dict) and ('_delete' in update or '_add' in update or '_generate' in update or
+                                             '_divide' in update):
+                update = self._structural(cpath, update)
+                current = parent.get(key, current)
             names = self._leaf_updaters.get(cpath)
             if names is None:
                 names = self._leaf_updaters[cpath] = {}
@@ -246,6 +273,128 @@ class Experiment:
         new = parent[key] = self.updaters[name](current, value, states)
         if isinstance(current, dict) or isinstance(new, dict):
             self._version += 1          # a branch was replaced: cached port nodes below it are stale
+
+    # -- structural updates (Store.apply_update, experiment.py:628-697) ----------------
+    def _structural(self, cpath, update):
+        """Apply the _delete / _add / _generate / _divide keys of an update at the
+        branch ``cpath``, in the reference's order; returns the rest of the update."""
+        if '_delete' in update:
+            for path in update['_delete']:
+                self._delete_path(cpath + tuple(path))
+        if '_add' in update:
+            for added in update['_add']:
+                self._add_path(cpath, tuple(added['path']), added['state'])
+        if '_generate' in update:
+            for g in update['_generate']:
+                self._generate(cpath, tuple(g['path']), g['processes'], g['topology'], g['initial_state'])
+        if '_divide' in update:
+            self._divide(cpath, update['_divide'])
+        return {k: v for k, v in update.items() if k not in ('_delete', '_add', '_generate', '_divide')}
+
+    def _structure_changed(self):
+        self._version += 1
+        self._structure += 1
+        self._updater_cache.clear()
+        self._leaf_updaters.clear()
+
+    def _establish(self, path):
+        node = self.state
+        for key in path:
+            if not isinstance(node.get(key), dict):
+                node[key] = {}
+            node = node[key]
+        return node
+
+    def _add_path(self, cpath, path, state):
+        path = normalize_path(cpath + path)
+        parent = self._establish(path[:-1])
+        if isinstance(parent.get(path[-1]), dict):
+            self._set_value(parent[path[-1]], state)
+        else:
+            parent[path[-1]] = _copy_tree(state)
+        self._structure_changed()
+
+    def _set_value(self, node, value):
+        """Store.set_value: keys the tree does not hold are ignored."""
+        for k, v in value.items():
+            if k not in node:
+                continue
+            if isinstance(node[k], dict) and isinstance(v, dict):
+                self._set_value(node[k], v)
+            else:
+                node[k] = _copy_tree(v)
+
+    def _generate(self, cpath, path, processes, topology, initial_state):
+        """Store.generate (experiment.py:1017-1029): the subtree at cpath + path, its
+        processes in the process tree, their topology, their ports' schemas."""
+        target = normalize_path(cpath + path)
+        node = self._establish(target)
+        pnode, tnode = self.processes, self.topology
+        for key in target[:-1]:
+            pnode = pnode.setdefault(key, {})
+            tnode = tnode.setdefault(key, {})
+        pnode.setdefault(target[-1], {}).update(processes)
+        tnode.setdefault(target[-1], {}).update(topology)
+        for ppath, proc in self._walk(processes, target):
+            for port, port_schema in proc.ports_schema().items():
+                self._register(self.port_path(ppath, port), port_schema)
+        self._set_value(node, initial_state or {})
+        self._structure_changed()
+
+    def _delete_path(self, path):
+        parent = self.get(path[:-1]) if path[:-1] else self.state
+        if path[-1] not in parent:
+            return
+        del parent[path[-1]]
+        pnode = self.processes
+        for key in path[:-1]:
+            pnode = pnode.get(key, {}) if isinstance(pnode, dict) else {}
+        if isinstance(pnode, dict) and path[-1] in pnode:
+            lost = pnode.pop(path[-1])
+            for _, proc in (self._walk(lost, ()) if isinstance(lost, dict) else [((), lost)]):
+                self._deleted.add(id(proc))
+                self._ports.pop(id(proc), None)
+        self._structure_changed()
+
+    def _divider_at(self, path):
+        if path in self.dividers:
+            return self.dividers[path]
+        for pat in self._div_globs:
+            if len(pat) == len(path) and all(p == '*' or p == q for p, q in zip(pat, path)):
+                return self.dividers[pat]
+        return None
+
+    def _divide_value(self, path, node):
+        """Store.divide_value (experiment.py:512-534)."""
+        div = self._divider_at(path)
+        if div is not None:
+            if isinstance(div, dict):
+                base = path[:-1]
+                states = {k: self.get(normalize_path(base + tuple(p))) for k, p in div['topology'].items()}
+                return div['divider'](node, states)
+            return (DIVIDERS[div] if isinstance(div, str) else div)(node)
+        if isinstance(node, dict):
+            daughters = [{}, {}]
+            for key, child in node.items():
+                division = self._divide_value(path + (key,), child)
+                if division:
+                    for daughter, value in zip(daughters, division):
+                        daughter[key] = value
+            return daughters
+        return None
+
+    def _divide(self, cpath, divide):
+        mother = divide['mother']
+        mpath = cpath + (mother,)
+        mstate = self.get(mpath)
+        initial_state = _copy_tree(mstate)
+        states = self._divide_value(mpath, mstate)
+        for daughter, state in zip(divide['daughters'], states):
+            initial_state = deep_merge(initial_state, state)
+            self._generate(cpath, tuple(daughter['path']), daughter['processes'], daughter['topology'],
+                           daughter['initial_state'])
+            self._set_value(self.get(cpath + (daughter['daughter'],)), initial_state)
+        self._delete_path(mpath)
 
     def _kinetics_plan(self, proc_path, process):
         """Where a BatchedConvenienceKinetics update lands, resolved once per
@@ -336,6 +485,8 @@ class Experiment:
         if derivers is None:
             derivers = [(p, s) for p, s in self._walk(self.processes, ()) if s.is_deriver()]
         for path, deriver in derivers:
+            if id(deriver) in self._deleted:          # removed by an earlier deriver's _divide / _delete
+                continue
             self.apply_update(deriver.next_update(0, self.process_states(path, deriver)), path)
 
     # -- Experiment.update (experiment.py:1351-1450) ---------------------------------
@@ -359,12 +510,17 @@ class Experiment:
         time = 0
         front = {}
         # the reference re-walks the tree every iteration (:1373-1380) because a
-        # _generate / _divide update can add processes; this store applies value
-        # updates only, so the tree is fixed for the call and is walked once
-        everything = self._walk(self.processes, ())
-        processes = [(p, s) for p, s in everything if not s.is_deriver()]
-        derivers = [(p, s) for p, s in everything if s.is_deriver()]
+        # _generate / _divide update can add processes; here it is walked again only
+        # after such an update moved the structure
+        seen = None
         while time < interval:
+            if seen != self._structure:
+                seen = self._structure
+                everything = self._walk(self.processes, ())
+                processes = [(p, s) for p, s in everything if not s.is_deriver()]
+                derivers = [(p, s) for p, s in everything if s.is_deriver()]
+                live = {p for p, _ in processes}
+                front = {p: f for p, f in front.items() if p in live}
             full_step = INFINITY
             for path, proc in processes:
                 if path not in front:

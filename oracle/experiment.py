@@ -16,6 +16,14 @@ A literal restatement, over nested dicts instead of Store objects, of
   * updaters accumulate / set / update_field_with_exchange .... vivarium/core/registry.py:117-183
   * topology paths relative to the process's parent, '..' steps up
     (normalize_path, experiment.py:1123-1130)
+  * structural updates at a branch, in Store.apply_update's order
+    (:628-697): _delete, _add, _generate (Store.generate :1017-1029) and
+    _divide (the mother's values deep-copied, Store.divide_value :512-534
+    with the schema's _divider per leaf -- registry.py:197-280 -- merged in
+    per daughter, daughters generated in order at the end of the branch, the
+    mother deleted, Store.delete_path :494-510); the loop walks the process
+    tree every iteration (:1373-1391) and skips derivers deleted earlier in
+    the same pass (:1321-1327)
 Processes are invoked immediately (InvokeProcess, :1157-1167).  A '*' key in
 a ports schema applies to every child of that store (DiffusionField's
 agents schema, diffusion_field.py:292-302).
@@ -23,7 +31,9 @@ agents schema, diffusion_field.py:292-302).
 
 from __future__ import annotations
 
+import copy
 import math
+import random
 
 import numpy as np
 
@@ -50,6 +60,51 @@ def update_set(current, new, states):
     return new
 
 
+def divide_set(state):
+    return [state, state]
+
+
+def divide_split(state):
+    if isinstance(state, (int, np.integer)) and not isinstance(state, bool):
+        remainder = state % 2
+        half = int(state / 2)
+        if random.choice([True, False]):
+            return [half + remainder, half]
+        else:
+            return [half, half + remainder]
+    elif state == float('inf') or state == 'Infinity':
+        return [state, state]
+    elif isinstance(state, (float, np.floating)):
+        half = state / 2
+        return [half, half]
+    raise Exception('can not divide state {} of type {}'.format(state, type(state)))
+
+
+def divide_zero(state):
+    return [0, 0]
+
+
+def divide_split_dict(state):
+    if state is None:
+        state = {}
+    d1 = dict(list(state.items())[len(state) // 2:])
+    d2 = dict(list(state.items())[:len(state) // 2])
+    return [d1, d2]
+
+
+DIVIDERS = {'set': divide_set, 'split': divide_split, 'split_dict': divide_split_dict, 'zero': divide_zero}
+
+
+def dict_merge(dct, merge_dct):
+    """vivarium/library/dict_utils.py deep_merge (mutates dct)."""
+    for k, v in merge_dct.items():
+        if k in dct and isinstance(dct[k], dict) and isinstance(v, dict):
+            dict_merge(dct[k], v)
+        else:
+            dct[k] = v
+    return dct
+
+
 def make_update_field_with_exchange(avogadro=N_A_LEGACY):
     def update_field_with_exchange(current, new, states):
         location = states['global']['location']
@@ -74,6 +129,8 @@ class OracleExperiment:
         self.updaters.update(updater_registry or {})
         self.schema = {}                      # store path (with '*' globs) -> updater name
         self._globs = []                      # the schema paths holding a '*'
+        self.dividers = {}                    # store path (with '*' globs) -> _divider
+        self.deleted = set()                  # ids of processes removed from the tree
         self.local_time = 0.0
         for path, proc in self._walk(processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -109,11 +166,13 @@ class OracleExperiment:
         if not isinstance(schema, dict):
             return
         keys = [k for k in schema if not k.startswith('_')]
-        if ('_default' in schema or '_value' in schema or '_updater' in schema) and not keys:
+        if ('_default' in schema or '_value' in schema or '_updater' in schema or '_divider' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
                 self.schema.setdefault(path, schema['_updater'])
                 if '*' in path and path not in self._globs:
                     self._globs.append(path)
+            if '_divider' in schema:
+                self.dividers.setdefault(path, schema['_divider'])
             if '*' not in path:
                 node = self.state
                 for key in path[:-1]:
@@ -147,7 +206,37 @@ class OracleExperiment:
         current = parent[path[-1]]
         inline = isinstance(update, dict) and '_updater' in update
         if isinstance(current, dict) and not inline:
+            if '_delete' in update:
+                for p in update['_delete']:
+                    self.delete_path(path + tuple(p))
+            if '_add' in update:
+                for added in update['_add']:
+                    target = normalize_path(path + tuple(added['path']))
+                    node = self.state
+                    for key in target[:-1]:
+                        node = node.setdefault(key, {})
+                    if isinstance(node.get(target[-1]), dict):
+                        self.set_value(node[target[-1]], added['state'])
+                    else:
+                        node[target[-1]] = copy.deepcopy(added['state'])
+            if '_generate' in update:
+                for g in update['_generate']:
+                    self.generate(path + tuple(g['path']), g['processes'], g['topology'], g['initial_state'])
+            if '_divide' in update:
+                divide = update['_divide']
+                mother = divide['mother']
+                mother_state = self.get(path + (mother,))
+                initial_state = copy.deepcopy(mother_state)
+                states = self.divide_value(path + (mother,), mother_state)
+                for daughter, state in zip(divide['daughters'], states):
+                    initial_state = dict_merge(initial_state, state)
+                    self.generate(path + tuple(daughter['path']), daughter['processes'], daughter['topology'],
+                                  daughter['initial_state'])
+                    self.set_value(self.get(path + (daughter['daughter'],)), copy.deepcopy(initial_state))
+                self.delete_path(path + (mother,))
             for key, value in update.items():
+                if key in ('_delete', '_add', '_generate', '_divide'):
+                    continue
                 self._apply(path + (key,), value, proc_path)
             return
         states = None
@@ -161,12 +250,77 @@ class OracleExperiment:
             name, value = self._updater_at(path), update
         parent[path[-1]] = self.updaters[name](current, value, states)
 
+    # -- structure ----------------------------------------------------------------
+    def set_value(self, node, value):
+        """Store.set_value: values for keys the tree holds; others ignored."""
+        for k, v in value.items():
+            if k in node:
+                if isinstance(node[k], dict) and isinstance(v, dict):
+                    self.set_value(node[k], v)
+                else:
+                    node[k] = v
+
+    def generate(self, target, processes, topology, initial_state):
+        target = normalize_path(target)
+        node = self.state
+        for key in target:
+            node = node.setdefault(key, {})
+        pnode, tnode = self.processes, self.topology
+        for key in target[:-1]:
+            pnode = pnode.setdefault(key, {})
+            tnode = tnode.setdefault(key, {})
+        pnode.setdefault(target[-1], {}).update(processes)
+        tnode.setdefault(target[-1], {}).update(topology)
+        for ppath, proc in self._walk(processes, target):
+            for port, port_schema in proc.ports_schema().items():
+                self._register(self.port_path(ppath, port), port_schema)
+        self.set_value(node, initial_state or {})
+
+    def delete_path(self, path):
+        parent = self.get(path[:-1])
+        if path[-1] in parent:
+            del parent[path[-1]]
+        pnode = self.processes
+        for key in path[:-1]:
+            pnode = pnode.get(key, {})
+        if path[-1] in pnode:
+            lost = pnode.pop(path[-1])
+            for _, proc in (self._walk(lost, ()) if isinstance(lost, dict) else [((), lost)]):
+                self.deleted.add(id(proc))
+
+    def divider_at(self, path):
+        if path in self.dividers:
+            return self.dividers[path]
+        for pat, div in self.dividers.items():
+            if '*' in pat and len(pat) == len(path) and all(p == '*' or p == q for p, q in zip(pat, path)):
+                return div
+        return None
+
+    def divide_value(self, path, node):
+        div = self.divider_at(path)
+        if div:
+            if isinstance(div, dict):
+                states = {k: self.get(normalize_path(path[:-1] + tuple(p))) for k, p in div['topology'].items()}
+                return div['divider'](node, states)
+            return (DIVIDERS[div] if isinstance(div, str) else div)(node)
+        if isinstance(node, dict):
+            daughters = [{}, {}]
+            for key, child in node.items():
+                division = self.divide_value(path + (key,), child)
+                if division:
+                    for daughter, divided in zip(daughters, division):
+                        daughter[key] = divided
+            return daughters
+        return None
+
     def send_updates(self, updates, derivers=None):
         for update, path in updates:
             self.apply_update(update, path)
         if derivers is None:
             derivers = [(p, s) for p, s in self._walk(self.processes, ()) if s.is_deriver()]
         for path, deriver in derivers:
+            if id(deriver) in self.deleted:
+                continue
             update = deriver.next_update(0, self.process_states(path, deriver))
             self.apply_update(update, path)
 

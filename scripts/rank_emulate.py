@@ -1,7 +1,9 @@
 """Per-rank cost of strong-scaled C4 diffusion on ONE GPU: a middle rank's row band
 (4096/N rows + halo rows both sides), 100 substeps per step in blocks of `halo`
 substeps, each block preceded by a local stand-in for the halo exchange (the
-same 4 row-copies per field the real exchange does; no RCCL).  Prints ms per step.
+same 4 row-copies per field the real exchange does; no RCCL).  The whole plane is
+timed live in the same process with the settings the one-GPU bench uses (34-row
+tiles), and the band is reported against 1/N of it.  Prints ms per step.
 
     python scripts/rank_emulate.py N halo rows [variant depth [mode]]     (mode: exact | fma)
 """
@@ -12,13 +14,33 @@ from lens_amd import configs
 from lens_amd.lattice import Lattice, stencil_depth, stencil_kernel
 from lens_amd.distributed import row_bands
 world, halo, rows = (int(x) for x in sys.argv[1:4])
-variant = int(sys.argv[4]) if len(sys.argv) > 4 else 3
-depth = int(sys.argv[5]) if len(sys.argv) > 5 else 9
-mode = sys.argv[6] if len(sys.argv) > 6 else 'exact'
+variant = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+depth = int(sys.argv[5]) if len(sys.argv) > 5 else 10
+mode = sys.argv[6] if len(sys.argv) > 6 else 'fma'
 from lens_amd.lattice import stencil_mode
 stencil_mode(mode)
 dev = torch.device('cuda', 0)
 nx = 4096
+
+
+def time_steps(fn, warm=20, reps=10):
+    for _ in range(warm):   # past the power-management transient after setup (profiles/r02g_eager_trace_gaps.log)
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps * 1e3
+
+
+glc0 = configs.gaussian_bump_field((nx, nx))
+whole = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev,
+                initial={'glc__D_e': glc0, 'ac_e': glc0 * 0.5})
+stencil_kernel(variant, 34)
+stencil_depth(depth)
+whole_ms = time_steps(lambda: whole.diffuse(1.0))
+del whole
 band = row_bands(nx, world)[1 if world > 2 else 0]
 glc = configs.gaussian_bump_field((nx, nx))
 lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev, row_band=band,
@@ -36,13 +58,7 @@ def fake_exchange(src, cnt):
         bufs[2].copy_(src[:, lat.row_hi - h:lat.row_hi]); bufs[3].copy_(bufs[2])
         src[:, lat.row_hi:lat.row_hi + h].copy_(bufs[3])
 
-for _ in range(20):   # past the power-management transient after setup (profiles/r02g_eager_trace_gaps.log)
-    lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(10):
-    lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
-torch.cuda.synchronize()
-ms = (time.perf_counter() - t0) / 10 * 1e3
-print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step (ideal %.3f = 1/N of the whole)' % (
-    world, band, halo, rows, variant, depth, mode, ms, 1.95 / world))
+ms = time_steps(lambda: lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None))
+print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step; whole plane %.3f ms (live), '
+      'ideal %.3f = 1/N of it, diffusion efficiency %.2f' % (world, band, halo, rows, variant, depth, mode, ms,
+                                                             whole_ms, whole_ms / world, whole_ms / world / ms))

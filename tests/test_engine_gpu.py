@@ -238,3 +238,96 @@ def test_colony_run_multirate_equals_reference_loop():
             assert np.array_equal(got[s], want), (interval, port, name)
         for f, m in enumerate(lat.molecules):
             assert np.array_equal(lat.owned(m).cpu().numpy(), ref.state['fields'][m]), (interval, m)
+
+
+def _dividing_colony(batched, dev, n=24, seed=4):
+    """growth_division_minimal's compartment (GrowthProtein + the MetaDivision
+    deriver, daughters regenerated from the same compartment) with the
+    convenience kinetics of the lattice colony above on every agent."""
+    from lens_amd import configs
+    from lens_amd.division import GrowthProtein, MetaDivision
+    from lens_amd.process import BatchedConvenienceKinetics, BatchedDiffusionField
+    from oracle.experiment import OracleConvenienceKinetics, OracleDiffusionField
+    from oracle.kinetics import mmol_to_counts
+    cfg = configs.glc_ac_config()
+    rng = np.random.default_rng(seed)
+    glc = configs.gaussian_bump_field((NX, NY))
+    env = {'molecules': ['glc__D_e', 'ac_e'], 'n_bins': [NX, NY], 'bounds': [float(NX), float(NY)],
+           'depth': 10.0, 'diffusion': 5.0, 'time_step': 2.0,
+           'initial_state': {'glc__D_e': glc, 'ac_e': np.zeros((NX, NY))}}
+
+    def compartment(agent_id):
+        kin_cfg = dict(cfg, time_step=1.0)
+        kin = BatchedConvenienceKinetics(kin_cfg) if batched else OracleConvenienceKinetics(kin_cfg)
+        return {'processes': {'kinetics': kin, 'growth': GrowthProtein({'growth_rate': 0.08}),
+                              'division': MetaDivision({'agent_id': agent_id, 'daughter_path': (),
+                                                        'compartment': lambda c: compartment(c['agent_id'])})},
+                'topology': {'kinetics': {'internal': ('internal',), 'external': ('boundary', 'external'),
+                                          'fluxes': ('fluxes',), 'fields': ('..', '..', 'fields'),
+                                          'dimensions': ('..', '..', 'dimensions'), 'global': ('boundary',)},
+                             'growth': {'internal': ('internal',), 'global': ('boundary',)},
+                             'division': {'global': ('boundary',), 'cells': ('..', '..', 'agents')}}}
+
+    processes = {'diffusion': BatchedDiffusionField(dict(env, device=dev)) if batched else OracleDiffusionField(env),
+                 'agents': {}}
+    topology = {'diffusion': {'agents': ('agents',), 'fields': ('fields',), 'dimensions': ('dimensions',)},
+                'agents': {}}
+    agents = {}
+    for a in range(n):
+        aid = str(a)
+        c = compartment(aid)
+        processes['agents'][aid], topology['agents'][aid] = c['processes'], c['topology']
+        internal = {k: v * (1 + 0.01 * a) for k, v in cfg['initial_state']['internal'].items()}
+        internal['protein'] = c['processes']['growth'].initial_protein * float(rng.uniform(1.0, 1.9))
+        agents[aid] = {'internal': internal, 'fluxes': {},
+                       'boundary': {'location': [float(rng.uniform(0, NX)), float(rng.uniform(0, NY))],
+                                    'mmol_to_counts': mmol_to_counts(1339.0 + a), 'volume': 1.0 + 0.01 * a,
+                                    'divide': False, 'external': {'glc__D_e': 0.0, 'ac_e': 0.0}}}
+    init = {'agents': agents,
+            'dimensions': {'bounds': env['bounds'], 'n_bins': env['n_bins'], 'depth': env['depth']}}
+    return processes, topology, init
+
+
+def test_dividing_colony_through_batched_loop_equals_reference_restatement():
+    """A growth_division_minimal-style colony (MetaDivision + GrowthProtein +
+    BatchedConvenienceKinetics under BatchedInvoke, Euler) on the device
+    lattice, through lens_amd.engine.Experiment, against the oracle loop
+    (oracle kinetics, numpy diffusion, one-agent exchange): agent ids, their
+    order, every agent state and both fields bit for bit after every interval,
+    with divisions along the way (daughters appended in mother order, mothers
+    deleted, their processes gone)."""
+    import random
+    from lens_amd.engine import Experiment
+    from lens_amd.invoke import BatchedInvoke
+    from oracle.experiment import OracleExperiment
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    intervals = (1.0, 3.0, 0.5, 4.5, 2.0, 5.0)
+
+    def run(batched):
+        np.random.seed(21)
+        random.seed(21)
+        p, t, init = _dividing_colony(batched, dev)
+        exp = (Experiment({'processes': p, 'topology': t, 'initial_state': init, 'invoke': BatchedInvoke(dev)})
+               if batched else OracleExperiment(p, t, init))
+        out = []
+        for interval in intervals:
+            exp.update(interval)
+            if batched:
+                torch.cuda.synchronize()
+            fields = {m: _to_host(v).copy() for m, v in exp.state['fields'].items()}
+            agents = {k: {port: dict(v) if isinstance(v, dict) else v for port, v in st.items()}
+                      for k, st in exp.state['agents'].items()}
+            out.append((exp.local_time, list(exp.state['agents']), agents, fields,
+                        sorted(exp.processes['agents'])))
+        return out
+
+    gpu, ref = run(True), run(False)
+    for k, (g, r) in enumerate(zip(gpu, ref)):
+        assert g[0] == r[0], k
+        assert g[1] == r[1], (k, g[1], r[1])
+        _compare(g[2], r[2], ('agents', k))
+        _compare(g[3], r[3], ('fields', k))
+        assert g[4] == r[4] == sorted(g[1])
+    assert len(gpu[-1][1]) > 24                                # divisions happened

@@ -120,3 +120,25 @@ def test_graph_replay_refuses_moved_agents(dev):
     with pytest.raises(RuntimeError):
         replay()
 
+
+
+def test_stamped_capture_equals_eager_and_stamps_are_ordered(dev):
+    """Colony.capture(..., stamps=...) -- the bench's instrumented replay that
+    splits a step into kinetics and the rest -- changes nothing: the replayed
+    steps equal eager steps bit for bit, and every step's three timestamps are
+    in order, the next step's first after its last."""
+    import numpy as np
+    from lens_amd import native
+    a = _lattice_colony(dev)
+    b = _lattice_colony(dev)
+    stamps = torch.zeros(3 * 4, dtype=torch.int64, device=dev)
+    replay = a.capture(1.0, 4, stamps=stamps)
+    replay()
+    for _ in range(4):
+        b.step(1.0)
+    torch.cuda.synchronize()
+    assert torch.equal(a.conc, b.conc)
+    assert torch.equal(a.lattice.fields, b.lattice.fields)
+    s = stamps.cpu().numpy().reshape(4, 3)
+    assert (np.diff(s, axis=1) > 0).all() and (s[1:, 0] > s[:-1, 2]).all()
+    assert native._lib.vk_wall_clock_khz() > 0
