@@ -12,6 +12,7 @@
 
 extern int g_stencil_rows;   // output rows per wave tile, 0 = auto (vk_lattice.hip, vk_set_stencil_kernel)
 extern int g_stencil_mode;   // 0 = bit-exact (default), 1 = tolerance / FMA (vk_set_stencil_mode)
+extern int g_stencil_stagger;  // pair-sum passes: odd tile columns' chunk grid shifted by half a chunk (variant 23)
 
 void vk_launch_wl3(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 3 rows prefetched
 void vk_launch_wl6(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 6 rows prefetched

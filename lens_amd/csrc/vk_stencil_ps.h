@@ -262,6 +262,7 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
+                                                    int stagger,
                                                     const double *__restrict__ uniform) {
     constexpr int KH = (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
     constexpr int W = 64 * C - 2 * KH;           // columns written per tile
@@ -272,8 +273,13 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     const int ty = (wave / tiles_x) % chunks_y;
     const int f = wave / (tiles_x * chunks_y);
     if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;     // uniform plane: zero delta
-    const int c0 = out_lo + ty * rows_per_chunk;
-    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    // stagger > 0: odd tile columns shift their chunk grid up by `stagger` rows
+    // (one chunk more, the first and last ones short), so the waves of a round
+    // do not run their fill phases in lockstep (chunks_y counts the extra one)
+    const int shift = (tx & 1) ? stagger : 0;
+    const int c0 = max(out_lo, out_lo + ty * rows_per_chunk - shift);
+    const int c1 = min(out_lo + (ty + 1) * rows_per_chunk - shift, out_hi);
+    if (c0 >= c1) return;
     const int x0 = tx * W;
     PsLane L;
     L.ny = ny;
@@ -321,7 +327,8 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     constexpr int W = 64 * C - 2 * KH;
     const int tiles_x = (ny + W - 1) / W;
     const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
-    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
+    const int sh = g_stencil_stagger ? rch / 2 : 0;
+    const int chunks_y = (out_hi - out_lo + rch - 1) / rch + (sh ? 1 : 0);
     const int waves = tiles_x * chunks_y * nf;
     const double c4 = 1.0 - 4.0 * coef;
     // the rescaled form while c4^-K stays far from overflow (|c4| >= 1e-3, i.e. coef
@@ -330,10 +337,10 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm);
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, sh, mm);
     } else {
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, sh, mm);
     }
 }
 
