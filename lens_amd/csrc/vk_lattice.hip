@@ -78,7 +78,8 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // Exact mode: 2 / 3 = wave tile lag-1 prefetching 3 / 6 rows, 6 = variant 3 with
 // streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
 // setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default),
-// 21 / 22 / 23 = its A/B alternates (2 / 6 rows prefetched; half-chunk stagger on odd tile columns),
+// 21 / 22 / 23 / 24 / 25 = its A/B alternates (2 / 6 rows prefetched; half-chunk stagger on odd tile
+// columns; cached stores; streaming loads),
 // 6 = the variant-6 FMA form (4 FP64 ops per cell-substep instead of 3).
 // Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
 // 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
@@ -90,7 +91,7 @@ int g_stencil_stagger = 0;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 23)) {
+    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 25)) {
         g_stencil_kernel = variant;
         g_stencil_stagger = variant == 23;
     }

@@ -62,13 +62,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *row, in
 // one tile wide, or a reflected row in reach): columns clamped per element and
 // stores masked per column.  Otherwise 16-B buffer accesses: a lane left or
 // right of the plane loads zeros (its columns are halo) and stores nothing.
-template <int C, bool CL>
+// CP (cache policy, A/B): bit 0 = streaming (nt) loads, bit 1 = plain (cached) stores; 0 = plain loads and
+// streaming stores (the default)
+template <int C, bool CL, int CP = 0>
 __device__ __forceinline__ void ps_load(double (&out)[C], const double *__restrict__ row, const PsLane &L) {
     if constexpr (!CL) {
         const __amdgpu_buffer_rsrc_t rs = row_rsrc(row, L.ny);
 #pragma unroll
         for (int j = 0; j < C; j += 2) {
-            const i4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(L.loff + 8u * j), 0, 0);
+            const i4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(L.loff + 8u * j), 0, (CP & 1) ? 2 : 0);
             const double2 y = __builtin_bit_cast(double2, x);
             out[j] = y.x;
             out[j + 1] = y.y;
@@ -79,7 +81,7 @@ __device__ __forceinline__ void ps_load(double (&out)[C], const double *__restri
     }
 }
 
-template <int C, bool CL>
+template <int C, bool CL, int CP = 0>
 __device__ __forceinline__ void ps_store(double *row, const double (&v)[C], const PsLane &L) {
     if constexpr (!CL) {
         // branch-free: a lane that does not write carries an out-of-range offset
@@ -88,7 +90,8 @@ __device__ __forceinline__ void ps_store(double *row, const double (&v)[C], cons
 #pragma unroll
         for (int j = 0; j < C; j += 2) {
             const double2 y = make_double2(v[j], v[j + 1]);
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, y), rs, (int)(L.voff + 8u * j), 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4v, y), rs, (int)(L.voff + 8u * j), 0,
+                                                   (CP & 2) ? 0 : 2);
         }
     } else {
 #pragma unroll
@@ -174,14 +177,14 @@ __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (in
 
 // Iteration i at ring phase U (row i sits in ring slot U): prefetch row i+PD,
 // run stages [0, ACT), store row i-K if STORE.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int ACT, bool STORE, int U>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U>
 __device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i) {
     constexpr int NR = PD + 2;
     constexpr int P = U & 1;
     // keep iterations in program order: the scheduler would otherwise hoist the
     // unrolled group's row loads (and their registers) to its top
     __builtin_amdgcn_sched_barrier(0);
-    ps_load<C, GL && GR && EY>(S.ring[(U + PD) % NR], A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
+    ps_load<C, GL && GR && EY, CP>(S.ring[(U + PD) % NR], A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
 #pragma unroll
     for (int q = 0; q < ACT; ++q) {
         const int r = i - 1 - q;
@@ -201,44 +204,44 @@ __device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, c
 #pragma unroll
                 for (int j = 0; j < C; ++j) v[j] *= A.cK;
             }
-            ps_store<C, GL && GR && EY>(A.d + (int64_t)(i - K) * L.ny64, v, L);
+            ps_store<C, GL && GR && EY, CP>(A.d + (int64_t)(i - K) * L.ny64, v, L);
         }
     }
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int T>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int T>
 __device__ __forceinline__ void ps_fill(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int is) {
     if constexpr (T < 2 * K - 1) {
         constexpr int ACT = T / 2 + 1 < K ? T / 2 + 1 : K;
-        ps_iter<K, PD, C, GL, GR, EY, SC, ACT, false, T % (PD + 2)>(S, A, L, is + T);
-        ps_fill<K, PD, C, GL, GR, EY, SC, T + 1>(S, A, L, is);
+        ps_iter<K, PD, C, GL, GR, EY, SC, CP, ACT, false, T % (PD + 2)>(S, A, L, is + T);
+        ps_fill<K, PD, C, GL, GR, EY, SC, CP, T + 1>(S, A, L, is);
     }
 }
 
 // The last (i1 - i) < NR iterations, nested (iteration u runs only if u-1 ran),
 // so that no state has to be merged across a skipped iteration: a flat list of
 // guarded iterations keeps both versions of every row live and costs ~60 VGPRs.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int PH, int u>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u>
 __device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n) {
     constexpr int NR = PD + 2;
     if constexpr (u < NR - 1) {
         if (u < n) {
-            ps_iter<K, PD, C, GL, GR, EY, SC, K, true, (PH + u) % NR>(S, A, L, i + u);
-            ps_tail<K, PD, C, GL, GR, EY, SC, PH, u + 1>(S, A, L, i, n);
+            ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + u) % NR>(S, A, L, i + u);
+            ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, u + 1>(S, A, L, i, n);
         }
     }
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int... Us>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int... Us>
 __device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsState<K, PD, C> &S, const PsArgs &A,
                                           const PsLane &L, int i, int i1) {
     constexpr int NR = PD + 2;
     constexpr int PH = (2 * K - 1) % NR;    // ring phase of the first steady iteration
-    for (; i + NR <= i1; i += NR) (ps_iter<K, PD, C, GL, GR, EY, SC, K, true, (PH + Us) % NR>(S, A, L, i + Us), ...);
-    ps_tail<K, PD, C, GL, GR, EY, SC, PH, 0>(S, A, L, i, i1 - i);
+    for (; i + NR <= i1; i += NR) (ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR>(S, A, L, i + Us), ...);
+    ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, 0>(S, A, L, i, i1 - i);
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP>
 __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1) {
     constexpr int NR = PD + 2;
     PsState<K, PD, C> S;
@@ -249,15 +252,15 @@ __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0
     // iteration `is` = c0-K+1 is stage 0's d-only step (d of row c0-K for its
     // first useful row c0-K+1); it reads row is-1 from slot NR-1, row is from slot 0
     const int is = c0 - K + 1;
-    ps_load<C, GL && GR && EY>(S.ring[NR - 1], A.s + clamp_row(is - 1, A.in_lo, A.in_hi) * L.ny64, L);
+    ps_load<C, GL && GR && EY, CP>(S.ring[NR - 1], A.s + clamp_row(is - 1, A.in_lo, A.in_hi) * L.ny64, L);
 #pragma unroll
-    for (int u = 0; u < PD; ++u) ps_load<C, GL && GR && EY>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
-    ps_fill<K, PD, C, GL, GR, EY, SC, 0>(S, A, L, is);
+    for (int u = 0; u < PD; ++u) ps_load<C, GL && GR && EY, CP>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
+    ps_fill<K, PD, C, GL, GR, EY, SC, CP, 0>(S, A, L, is);
     // steady: i = c0+K .. c1+K-1, one stored row each (rows c0 .. c1-1)
-    ps_steady<K, PD, C, GL, GR, EY, SC>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);
+    ps_steady<K, PD, C, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);
 }
 
-template <int K, int PD, int C, bool SC>
+template <int K, int PD, int C, bool SC, int CP = 0>
 __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
@@ -315,12 +318,12 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     // fix each) took the kernel past 168 VGPRs (2 waves per SIMD); the unscaled
     // form (coef ~ 1/4) runs the general body everywhere.
     if (!SC || ey || gl || gr || (ny % C) != 0)
-        ps_body<K, PD, C, true, true, true, SC>(A, L, c0, c1);
+        ps_body<K, PD, C, true, true, true, SC, CP>(A, L, c0, c1);
     else if constexpr (SC)
-        ps_body<K, PD, C, false, false, false, SC>(A, L, c0, c1);
+        ps_body<K, PD, C, false, false, false, SC, CP>(A, L, c0, c1);
 }
 
-template <int K, int PD, int C>
+template <int K, int PD, int C, int CP = 0>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
             int in_lo, int in_hi, int top, int bot, double coef, const double *mm) {
     constexpr int KH = (K + C - 1) / C * C;
@@ -336,10 +339,10 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     if (fabs(c4) >= 1e-3) {
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
                            out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, sh, mm);
     } else {
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, sh, mm);
     }
 }
