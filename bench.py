@@ -113,6 +113,9 @@ def parse(argv=None):
     p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
                    help='replay the timed steps from a captured HIP graph (auto: every single-GPU step that takes '
                         'no host decision, i.e. no division: C2, C3, C4)')
+    p.add_argument('--steps-per-launch', type=int, default=None,
+                   help='held colonies (C2): timesteps per kernel launch (vk_step_dopri5_multi, each step bit for '
+                        'bit the one-step kernel\'s); default = the steps per replayed graph')
     p.add_argument('--settle-ms', type=float, default=30.0,
                    help='after the W warmup steps, run more untimed steps until the warmup has kept the GPU '
                         'busy this long (power-management transient, profiles/r02g_eager_trace_gaps.log); '
@@ -520,7 +523,14 @@ def main():
                       'graphs_per_step': 1 + len(banded_step.graphs[1])}
     elif use_graph:
         per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
-        replay = col.capture(1.0, per_graph)
+        # a held colony's agents do not couple between steps: a graph of 10 steps is
+        # one launch of 10 steps (vk_step_dopri5_multi) instead of 10 launches
+        multi_ok = (lat is None and col.cells is None and col.integrator == 'dopri5' and
+                    col.engine.default_variant() == 2)
+        spl = args.steps_per_launch if args.steps_per_launch is not None else (per_graph if multi_ok else 1)
+        if spl > 1 and (not multi_ok or per_graph % spl):
+            raise SystemExit('--steps-per-launch: a held DP45 colony, dividing the %d steps per graph' % per_graph)
+        replay = col.capture(1.0, per_graph, steps_per_launch=spl)
         replay()             # uploads the graph; its steps are warmup, not timed
         barrier()
         col.check_status()
@@ -541,7 +551,7 @@ def main():
             barrier()
             settle_steps += (1 + int(need.item())) * per_graph
         graph_info = {'steps_per_graph': per_graph, 'replays': args.steps // per_graph,
-                      'untimed_warmup_replay_steps': per_graph}
+                      'untimed_warmup_replay_steps': per_graph, 'steps_per_launch': spl}
     agent_steps = 0          # agents integrated, summed over the timed steps (divisions grow n)
     n_start = col.n
     if divides:

@@ -160,6 +160,22 @@ int vk_step_dopri5(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
                    double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
                    vk_stream_t stream);
 
+/* n_steps consecutive agent-steps of dt in one launch, for colonies whose
+ * agents do not couple between steps (held externals; BASELINE config 2):
+ * every step is vk_step_dopri5 variant 2's, bit for bit, with the state kept
+ * in registers between steps.  Step s writes its mean fluxes at flux + s *
+ * step_flux, its exchange counts at counts + s * step_counts and its attempts
+ * at nsteps + s * step_nsteps (rows of ld, as vk_step_dopri5); conc and
+ * h_state hold the end state, status ORs every step's bits.  Needs
+ * vk_table_specialize with an agent-per-lane source.  Not a reference
+ * interface: the reference steps agents one Delta t at a time
+ * (Experiment.update, experiment.py:1351-1450).                            */
+int vk_step_dopri5_multi(const vk_table *t, int64_t n_agents, int64_t ld, double dt, int32_t n_steps,
+                         const vk_ode_opts *opts, const double *params, double *conc, const double *m2c,
+                         double *h_state, double *flux, int64_t step_flux, int64_t *counts,
+                         int64_t step_counts, int32_t *status, int32_t *nsteps, int64_t step_nsteps,
+                         vk_stream_t stream);
+
 /* Lattice fields: n_fields planes of rows x ny doubles, plane stride
  * field_stride.  Local rows may include halo rows of neighbouring ranks.   */
 

@@ -267,6 +267,35 @@ class Colony:
             if getattr(self, 'attempts', None) is not None:
                 self.attempts += self.nsteps[:self.n].sum()
 
+    def _step_buffers(self, k):
+        t, ld = self.table, self.ld
+        if getattr(self, 'flux_steps', None) is None or self.flux_steps.shape[0] != k:
+            self.flux_steps = torch.zeros((k, t.n_reactions, ld), dtype=torch.float64, device=self.device)
+            self.counts_steps = torch.zeros((k, t.n_ext, ld), dtype=torch.int64, device=self.device)
+            self.nsteps_steps = torch.zeros((k, ld), dtype=torch.int32, device=self.device)
+            self._layout += 1
+
+    def step_many(self, dt: float = 1.0, steps: int = 1):
+        """``steps`` timesteps of a colony whose agents do not couple between
+        steps (environment 'held', no cells, DP45 with the specialised kernel)
+        in ONE launch (vk_step_dopri5_multi): each step equals :meth:`step`
+        bit for bit.  Every step's fluxes, exchange counts and attempts stay in
+        ``flux_steps`` [steps, R, ld], ``counts_steps`` [steps, E, ld] and
+        ``nsteps_steps`` [steps, ld]; ``flux`` / ``counts`` / ``nsteps`` view
+        the last step's."""
+        if self.environment != 'held' or self.cells is not None or self.integrator != 'dopri5':
+            raise ValueError('step_many: held externals, no division, DP45 (agents must not couple between steps)')
+        k = int(steps)
+        self._step_buffers(k)
+        self.engine.dopri5_multi(dt, k, self.params, self.conc, self.m2c, self.n, self.h_state, self.rtol,
+                                 self.atol, self.max_steps, self.flux_steps, self.counts_steps, self.status,
+                                 self.nsteps_steps)
+        self.flux, self.counts, self.nsteps = self.flux_steps[k - 1], self.counts_steps[k - 1], self.nsteps_steps[k - 1]
+        if getattr(self, 'attempts', None) is not None:
+            self.attempts += self.nsteps_steps[:, :self.n].sum()
+        self.time += dt * k
+        self.step_index += k
+
     def step(self, dt: float = 1.0, halo_exchange=None, allreduce=None, timing=None, stamp=None):
         """One timestep.  ``timing`` (optional) = {'kin': (ev0, ev1), 'diff': (ev0, ev1)}
         of torch.cuda.Events recorded on the launch stream around those kernels.
@@ -423,7 +452,7 @@ class Colony:
                 lat.exchange_atomic(self.bin_lin, self.n, self.counts, self.map_exch_count,
                                     self.map_exch_field)
 
-    def capture(self, dt: float = 1.0, steps: int = 1, stamps=None):
+    def capture(self, dt: float = 1.0, steps: int = 1, stamps=None, steps_per_launch: int = 1):
         """Capture ``steps`` timesteps into one HIP graph (torch.cuda.CUDAGraph)
         and return a function that replays them.
 
@@ -440,6 +469,8 @@ class Colony:
         holds the buffers and the agent count of capture time: set_agents()
         values may change between replays (they are copied in place), but a
         re-binning of moved agents invalidates it (replay raises).
+        ``steps_per_launch`` > 1 (a held colony without division) captures
+        :meth:`step_many` launches of that many steps instead.
         ``stamps`` (optional, a device int64 tensor of 3 * steps) records each
         replayed step's segment boundaries (:meth:`step`'s ``stamp``) at
         [3k, 3k + 1, 3k + 2] -- vk_timestamp ticks, vk_wall_clock_khz per ms."""
@@ -451,11 +482,18 @@ class Colony:
                              'capture_banded)')
         if steps < 1:
             raise ValueError('Colony.capture: steps >= 1')
+        spl = int(steps_per_launch)
+        if spl > 1 and (stamps is not None or steps % spl):
+            raise ValueError('Colony.capture: steps_per_launch must divide steps (and takes no stamps)')
+        if spl > 1:
+            self._step_buffers(spl)                 # allocated before the capture (graphs hold the pointers)
         graph = torch.cuda.CUDAGraph()
         t0, s0 = self.time, self.step_index
         layout, n = self._layout, self.n
         with torch.cuda.graph(graph):
-            for k in range(steps):
+            for k in range(steps // spl if spl > 1 else 0):
+                self.step_many(dt, spl)
+            for k in range(steps if spl == 1 else 0):
                 stamp = None
                 if stamps is not None:
                     stamp = (lambda tag, k=k: native.check(native._lib.vk_timestamp(

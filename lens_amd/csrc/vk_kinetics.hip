@@ -208,9 +208,10 @@ extern "C" int vk_table_specialize(vk_table *t, const char *source) {
     int rc = vk::hip_check(hipModuleLoadData(&mod, code.data()), "hipModuleLoadData(spec)");
     if (rc) return rc;
     // the source defines the agent-per-lane kernel, the agent-per-wavefront one, or both
-    hipFunction_t fn = nullptr, fw = nullptr;
+    hipFunction_t fn = nullptr, fw = nullptr, fm = nullptr;
     if (hipModuleGetFunction(&fn, mod, "vk_dopri5_spec") != hipSuccess) fn = nullptr;
     if (hipModuleGetFunction(&fw, mod, "vk_dopri5_wspec") != hipSuccess) fw = nullptr;
+    if (hipModuleGetFunction(&fm, mod, "vk_dopri5_spec_multi") != hipSuccess) fm = nullptr;
     (void)hipGetLastError();
     if (!fn && !fw) {
         (void)hipModuleUnload(mod);
@@ -221,6 +222,7 @@ extern "C" int vk_table_specialize(vk_table *t, const char *source) {
     t->spec_module = mod;
     t->spec_dopri5 = fn;
     t->spec_wave = fw;
+    t->spec_multi = fm;
     return VK_OK;
 }
 
@@ -992,6 +994,42 @@ static int launch_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, co
     hipLaunchKernelGGL(k_dopri5_thread<NY>, dim3(blocks), dim3(DP_BS), lds, stream, t->dev, n, ld, dt, o->rtol,
                        o->atol, o->max_steps, params, conc, m2c, delta, h_state, flux, counts, status, nsteps);
     return vk::launch_check("k_dopri5_thread");
+}
+
+// n_steps agent-steps of dt per launch for agents that do not couple between
+// steps (held externals), with the network-specialised agent-per-lane kernel.
+extern "C" int vk_step_dopri5_multi(const vk_table *t, int64_t n, int64_t ld, double dt, int32_t n_steps,
+                                    const vk_ode_opts *o, const double *params, double *conc, const double *m2c,
+                                    double *h_state, double *flux, int64_t step_flux, int64_t *counts,
+                                    int64_t step_counts, int32_t *status, int32_t *nsteps, int64_t step_nsteps,
+                                    vk_stream_t stream) {
+    int rc = check_agents("vk_step_dopri5_multi", t, n, ld);
+    if (rc || n == 0 || n_steps == 0) return rc;
+    if (!o || !params || !conc || !m2c || !flux || (!counts && t->dev.n_ext > 0) || n_steps < 0) {
+        vk::set_error("vk_step_dopri5_multi: null argument or negative step count");
+        return VK_ERR_ARG;
+    }
+    if (!(dt > 0.0) || !(o->rtol > 0.0) || !(o->atol >= 0.0) || o->max_steps <= 0) {
+        vk::set_error("vk_step_dopri5_multi: need dt > 0, rtol > 0, atol >= 0, max_steps > 0");
+        return VK_ERR_ARG;
+    }
+    if (!t->spec_multi) {
+        vk::set_error("vk_step_dopri5_multi: needs vk_table_specialize with an agent-per-lane source first");
+        return VK_ERR_ARG;
+    }
+    if (n_steps > 1 && (step_flux < (int64_t)t->dev.n_reactions * ld || step_counts < (int64_t)t->dev.n_ext * ld ||
+                        (nsteps && step_nsteps < ld))) {
+        vk::set_error("vk_step_dopri5_multi: per-step output strides overlap");
+        return VK_ERR_ARG;
+    }
+    double rtol = o->rtol, atol = o->atol;
+    int max_steps = o->max_steps, k = n_steps;
+    void *args[] = {&n, &ld, &dt, &k, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c,
+                    &h_state, &flux, &step_flux, &counts, &step_counts, &status, &nsteps, &step_nsteps};
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    return vk::hip_check(hipModuleLaunchKernel(t->spec_multi, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream, args,
+                                               nullptr),
+                         "hipModuleLaunchKernel(vk_dopri5_spec_multi)");
 }
 
 extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,

@@ -171,6 +171,42 @@ class KineticsEngine:
         return flux, counts, status, nsteps
 
     # -- flop accounting (counted as the kernels execute) -----
+    def dopri5_multi(self, dt, n_steps, params, conc, mmol_to_counts, n_agents=None, h_state=None, rtol=1e-8,
+                     atol=1e-12, max_steps=100000, flux=None, counts=None, status=None, nsteps=None):
+        """``n_steps`` consecutive DP5(4) agent-steps of ``dt`` in one launch
+        (vk_step_dopri5_multi; agents that do not couple between steps, after
+        :meth:`specialize`).  ``flux`` [n_steps, n_reactions, ld], ``counts``
+        [n_steps, n_ext, ld] and ``nsteps`` [n_steps, ld] receive every step's
+        outputs; ``conc`` / ``h_state`` the end state.  Each step equals one
+        :meth:`dopri5` call (variant 2) bit for bit.  Returns (flux, counts,
+        status, nsteps)."""
+        t = self.table
+        if self.default_variant() != 2:
+            raise native.NativeError('dopri5_multi needs the specialised agent-per-lane kernel (specialize())')
+        k = int(n_steps)
+        n = conc.shape[1] if n_agents is None else n_agents
+        ld = self._check_state(params, conc, n)
+        _need(mmol_to_counts, 'mmol_to_counts', None, ld, F64, self.device)
+        flux = torch.empty((k, t.n_reactions, ld), dtype=F64, device=self.device) if flux is None else flux
+        counts = torch.empty((k, t.n_ext, ld), dtype=torch.int64, device=self.device) if counts is None else counts
+        status = self.empty_like_agents(None, ld, torch.int32) if status is None else status
+        nsteps = torch.empty((k, ld), dtype=torch.int32, device=self.device) if nsteps is None else nsteps
+        for name, x, shape, dtype in (('flux', flux, (k, t.n_reactions, ld), F64),
+                                      ('counts', counts, (k, t.n_ext, ld), torch.int64),
+                                      ('nsteps', nsteps, (k, ld), torch.int32)):
+            if tuple(x.shape) != shape or x.dtype != dtype or not x.is_contiguous() or x.device != self.device:
+                raise ValueError('%s must be a contiguous %s %s tensor on %s' % (name, shape, dtype, self.device))
+        _need(status, 'status', None, ld, torch.int32, self.device)
+        if h_state is not None:
+            _need(h_state, 'h_state', None, ld, F64, self.device)
+        opts = native.VkOdeOpts(float(rtol), float(atol), int(max_steps), 2)
+        native.check(native._lib.vk_step_dopri5_multi(
+            self.dev.handle, n, ld, float(dt), k, ctypes.byref(opts), native.ptr(params), native.ptr(conc),
+            native.ptr(mmol_to_counts), native.ptr(h_state), native.ptr(flux), t.n_reactions * ld,
+            native.ptr(counts), t.n_ext * ld, native.ptr(status), native.ptr(nsteps), ld,
+            native.stream_handle()), 'vk_step_dopri5_multi')
+        return flux, counts, status, nsteps
+
     def dopri5_flops_per_attempt(self) -> int:
         """6 RHS evaluations + stage combinations + error norm per attempted step."""
         ny = self.table.n_dyn + self.table.n_reactions

@@ -18,12 +18,12 @@ def dev():
     return torch.device('cuda', 0)
 
 
-def _colony(dev, n=5000):
+def _colony(dev, n=5000, specialize=False):
     from lens_amd.colony import Colony
     cfg = configs.glc_lct_config()
     t = compile_rate_laws(cfg['reactions'], cfg['kinetic_parameters'])
     params, conc = configs.heterogeneous_colony(t, cfg, n)
-    col = Colony(cfg, n, device=dev, integrator='dopri5', table=t)
+    col = Colony(cfg, n, device=dev, integrator='dopri5', table=t, specialize=specialize)
     col.set_agents(params=params, conc=conc)
     col.count_attempts(True)
     return col
@@ -142,3 +142,32 @@ def test_stamped_capture_equals_eager_and_stamps_are_ordered(dev):
     s = stamps.cpu().numpy().reshape(4, 3)
     assert (np.diff(s, axis=1) > 0).all() and (s[1:, 0] > s[:-1, 2]).all()
     assert native._lib.vk_wall_clock_khz() > 0
+
+
+@pytest.mark.parametrize('k', [1, 3, 10])
+def test_multi_step_launch_equals_single_steps(dev, k):
+    """Colony.step_many (vk_step_dopri5_multi): k held-colony steps in one
+    launch equal k single steps bit for bit -- state, carried step size, and
+    every step's fluxes, exchange counts and attempts -- also replayed from a
+    graph (the C2 bench's form)."""
+    a, b, c = (_colony(dev, specialize=True) for _ in range(3))
+    flux, counts, nsteps = [], [], []
+    for _ in range(2 * k):
+        b.step(1.0)
+        flux.append(b.flux[:, :b.n].clone())
+        counts.append(b.counts[:, :b.n].clone())
+        nsteps.append(b.nsteps[:b.n].clone())
+    for rep in range(2):
+        a.step_many(1.0, k)
+        for s in range(k):
+            assert torch.equal(a.flux_steps[s, :, :a.n], flux[rep * k + s])
+            assert torch.equal(a.counts_steps[s, :, :a.n], counts[rep * k + s])
+            assert torch.equal(a.nsteps_steps[s, :a.n], nsteps[rep * k + s])
+    assert torch.equal(a.conc, b.conc) and torch.equal(a.h_state, b.h_state)
+    assert torch.equal(a.flux, b.flux) and torch.equal(a.counts[:, :a.n], b.counts[:, :b.n])
+    replay = c.capture(1.0, 2 * k, steps_per_launch=k)
+    replay()
+    torch.cuda.synchronize()
+    assert torch.equal(c.conc, b.conc) and torch.equal(c.h_state, b.h_state)
+    a.check_status()
+    c.check_status()
