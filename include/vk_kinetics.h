@@ -216,6 +216,31 @@ int vk_diffuse_delta(double *field, double *work0, double *work1, double *delta,
                      int32_t sub_count, int32_t n_sub, double coeff_dt, const double *uniform,
                      vk_stream_t stream);
 
+/* One whole-plane step of n_sub substeps (rows [0, rows), both edges
+ * reflected) with the agent coupling carried by its passes -- one launch per
+ * pass instead of vk_gather + the passes + vk_exchange_sorted, same results:
+ *   - the first pass, before it changes anything, sets
+ *       conc[gather_row[f]*conc_ld + a] = plane f at bin_lin[a]   (vk_gather)
+ *   - the final pass, after writing plane f, adds
+ *       counts[count_row[f]*counts_ld + a] / binvol_avogadro * 1000
+ *     for the agents of each bin in agent order             (vk_exchange_sorted)
+ * gather_row / count_row: host arrays of n_fields rows (-1 = none).  Agents
+ * must be stored in bin order (bin_lin ascending, Colony.sort_by_bin), and
+ * seg[r*nseg + s] (nseg = (ny+15)/16) = the first agent whose bin_lin >= r*ny + 16 s.
+ * Uniform planes (the vk_field_uniform summary in `uniform`, nullable) keep
+ * their values and still gather and exchange.  Returns VK_ERR_LIMIT and launches
+ * nothing unless the step is planned as two or more pair-sum passes (the
+ * tolerance mode, vk_set_stencil_mode(1), with kernel variants 20-25 and pass
+ * depths 3..11; n_fields <= 8): the caller then runs the three steps itself.
+ * Not a reference interface: DiffusionField.next_update (diffusion_field.py:
+ * 362-407) and the agents' exchange updates (registry.py:149-183) fused.     */
+int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fields,
+                       int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
+                       const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
+                       int64_t n_agents, const int32_t *gather_row, double *conc, int64_t conc_ld,
+                       const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
+                       double binvol_avogadro, vk_stream_t stream);
+
 /* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
  * 1..15; 1 = one launch per substep; default 9; or 10: a tolerance-mode whole
  * step of a multiple of 10 substeps as 10-deep passes over three buffers).

@@ -37,7 +37,7 @@ from lens_amd import native
 from lens_amd.cells import CellModel, lineage_ids
 from lens_amd.configs import initial_conc
 from lens_amd.kinetics import KineticsEngine
-from lens_amd.lattice import Lattice, occupancy, N_A_LEGACY
+from lens_amd.lattice import Lattice, occupancy, segment_index, N_A_LEGACY
 from lens_amd.rate_law_compiler import compile_rate_laws, RateLawTable
 
 
@@ -69,6 +69,11 @@ class Colony:
         # banded lattices: the first halo exchange of a step runs on a comm stream
         # beside the kinetics and the gather (it writes only halo rows)
         self.overlap_halo = True
+        # lattice colonies stored in bin order: the gather and the exchange ride on
+        # the first and final diffusion passes (vk_diffuse_coupled; same results)
+        self.fuse_coupling = True
+        self._couple = None
+        self.last_step_coupled = False
         self._comm_stream = torch.cuda.Stream(self.device) if self.device.type == 'cuda' else None
         self.engine = KineticsEngine(self.table, self.device)
         if specialize and integrator == 'dopri5':
@@ -201,7 +206,38 @@ class Colony:
             raise ValueError('agents outside this rank\'s row band: attach a distributed.AgentRouter '
                              '(division moves daughters across band edges)')
         self.occ = occupancy(self.bin_lin, self.n, getattr(self, 'agent_order', None))
+        self._update_coupling()
         self._layout += 1            # captured graphs hold the old occupancy buffers
+
+    def _update_coupling(self):
+        """The segment index of the coupled passes (vk_diffuse_coupled), kept only
+        while the agents are stored in bin order on a whole, unbanded plane and
+        each plane gathers into / takes counts from at most one SoA row."""
+        self._couple = None
+        lat, n = self.lattice, self.n
+        if lat is None or self.cells is not None or self.router is not None or n == 0:
+            return
+        if lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot):
+            return
+        # stored in bin order, and within a bin in the exchange's agent order
+        # (occupancy: agent_order after sort_by_bin, else the column order)
+        b = self.bin_lin[:n].to(torch.int64)
+        key = getattr(self, 'agent_order', None)
+        if n > 1:
+            same = b[1:] == b[:-1]
+            ok = (b[1:] > b[:-1]) | (same & (key[1:n] > key[:n - 1]) if key is not None else same)
+            if not bool(ok.all()):
+                return
+        nf = len(lat.molecules)
+        rows = []
+        for fields, srcs in ((self.map_gather_field, self.map_gather_row), (self.map_exch_field, self.map_exch_count)):
+            r = [-1] * nf
+            for f, x in zip(fields.tolist(), srcs.tolist()):
+                if r[f] != -1:
+                    return
+                r[f] = x
+            rows.append(r)
+        self._couple = (segment_index(self.bin_lin, n, lat.rows_local, lat.ny), rows[0], rows[1])
 
     def sort_by_bin(self):
         """Store the agents in bin order, so that the exchange scatter and the
@@ -233,6 +269,7 @@ class Colony:
                 t[:, :n] = t[:, :n][:, perm]
         self.agent_order = key[perm]
         self.occ = occupancy(self.bin_lin, n, self.agent_order)
+        self._update_coupling()
         self._layout += 1            # captured graphs hold the old occupancy buffers
         return self.agent_order
 
@@ -340,12 +377,13 @@ class Colony:
             stamp(1)
         if self.lattice is not None:
             lat = self.lattice
-            self.gather_external()                       # pre-step field (one-step lag)
-            if halo_done is not None:
-                torch.cuda.current_stream(self.device).wait_event(halo_done)
-            lat.diffuse(dt, halo_exchange=halo_exchange, allreduce=allreduce,
-                        events=timing.get('diff'), halo_ready=halo_done is not None)
-            self._step_exchange()
+            if not (halo_done is None and halo_exchange is None and self._coupled_step(dt, allreduce, timing)):
+                self.gather_external()                       # pre-step field (one-step lag)
+                if halo_done is not None:
+                    torch.cuda.current_stream(self.device).wait_event(halo_done)
+                lat.diffuse(dt, halo_exchange=halo_exchange, allreduce=allreduce,
+                            events=timing.get('diff'), halo_ready=halo_done is not None)
+                self._step_exchange()
         elif self.environment == 'nonspatial':
             if self.map_exch_count.numel():
                 native.check(native._lib.vk_exchange_atomic(
@@ -442,6 +480,19 @@ class Colony:
         self.flux.copy_(flux)
         self.counts.copy_(counts)
         self._step_exchange()
+
+    def _coupled_step(self, dt, allreduce, timing):
+        """gather + diffusion + exchange as one coupled pass sequence, when the
+        colony and the plan allow it (vk_diffuse_coupled); False: nothing ran."""
+        cp, lat = self._couple, self.lattice
+        self.last_step_coupled = False
+        if (cp is None or not self.fuse_coupling or self.exchange_mode != 'sorted' or
+                not lat.coupled_plan_ok(dt)):
+            return False
+        seg, grow, crow = cp
+        self.last_step_coupled = lat.diffuse_coupled(dt, self.bin_lin, self.n, seg, grow, self.conc, crow,
+                                                     self.counts, allreduce=allreduce, events=timing.get('diff'))
+        return self.last_step_coupled
 
     def _step_exchange(self):
         lat = self.lattice

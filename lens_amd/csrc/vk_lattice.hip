@@ -79,7 +79,7 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
 // setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default),
 // 21 / 22 / 23 / 24 / 25 = its A/B alternates (2 / 6 rows prefetched; half-chunk stagger on odd tile
-// columns; cached stores; streaming loads),
+// columns; cached stores; streaming loads), 26 / 27 = 24 / 20 one plane at a time (depth-10 plans),
 // 6 = the variant-6 FMA form (4 FP64 ops per cell-substep instead of 3).
 // Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
 // 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
@@ -91,7 +91,7 @@ int g_stencil_stagger = 0;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 25)) {
+    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 27)) {
         g_stencil_kernel = variant;
         g_stencil_stagger = variant == 23;
     }
@@ -201,19 +201,25 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         // writes the field without reading it back (no f0), so the field is a third
         // buffer: pass p reads `cur` and writes the work buffer it did not read, and the
         // last pass writes the field.  Uniform planes skip every pass and keep their field.
-        const double *cur = field;
-        for (int j = 0, p = 0; j < n_sub; j += 10, ++p) {
-            const int e = j + 9;
-            const int grow = last_in_call - e;
-            const int lo = max(lo_min, row_lo - grow);
-            const int hi = min(hi_max, row_hi + grow);
-            const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
-            double *dst = (e == n_sub - 1) ? field : (cur == work0 ? work1 : work0);
-            launch_fast10(s, cur, dst, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
-                          coeff_dt, uniform);
-            int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
-            if (rc) return rc;
-            cur = dst;
+        // variants 26 / 27: one plane at a time, its passes back to back
+        const int nfl = g_stencil_kernel >= 26 ? 1 : n_fields;
+        for (int f = 0; f < n_fields; f += nfl) {
+            const int64_t off = (int64_t)f * field_stride;
+            double *pf = field + off, *w0 = work0 + off, *w1 = work1 + off;
+            const double *cur = pf;
+            for (int j = 0, p = 0; j < n_sub; j += 10, ++p) {
+                const int e = j + 9;
+                const int grow = last_in_call - e;
+                const int lo = max(lo_min, row_lo - grow);
+                const int hi = min(hi_max, row_hi + grow);
+                const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
+                double *dst = (e == n_sub - 1) ? pf : (cur == w0 ? w1 : w0);
+                launch_fast10(s, cur, dst, nfl, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
+                              coeff_dt, uniform ? uniform + 2 * f : nullptr);
+                int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
+                if (rc) return rc;
+                cur = dst;
+            }
         }
         return VK_OK;
     }
@@ -283,6 +289,108 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             if (rc) return rc;
         }
         j += k;
+    }
+    return VK_OK;
+}
+
+// A whole-plane step's passes with the agent coupling inside them: the first
+// pass also gathers each agent's external concentrations from the pre-step
+// planes, the final pass also scatters the exchange into the new planes (one
+// launch each less, and the exchange's read-modify-write of the planes happens
+// while the final pass holds them).  Returns VK_ERR_LIMIT, launching nothing,
+// when the step is not planned as two or more pair-sum passes.
+extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fields,
+                                  int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
+                                  const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
+                                  int64_t n_agents, const int32_t *gather_row, double *conc, int64_t conc_ld,
+                                  const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
+                                  double binvol_avogadro, vk_stream_t stream) {
+    if (!field || !work0 || !work1 || n_fields < 1 || ny <= 0 || rows <= 0 || n_sub < 0 ||
+        (int64_t)rows * ny > field_stride || (int64_t)rows * ny >= INT32_MAX || n_agents < 0 ||
+        n_agents >= INT32_MAX || nseg != (ny + 15) / 16 || (n_agents > 0 && (!bin_lin || !seg)) || !gather_row ||
+        !count_row) {
+        vk::set_error("vk_diffuse_coupled: bad arguments");
+        return VK_ERR_ARG;
+    }
+    VkPsCouple cp = {};
+    cp.bins = bin_lin;
+    cp.seg = seg;
+    cp.nseg = nseg;
+    cp.n = (int32_t)n_agents;
+    cp.gdst = conc;
+    cp.gld = conc_ld;
+    cp.counts = counts;
+    cp.cld = counts_ld;
+    cp.bva = binvol_avogadro;
+    if (n_fields <= VK_COUPLE_MAX_FIELDS) {
+        for (int f = 0; f < n_fields; ++f) {
+            if (gather_row[f] >= 127 || count_row[f] >= 127 || (gather_row[f] >= 0 && (!conc || conc_ld < n_agents)) ||
+                (count_row[f] >= 0 && (!counts || counts_ld < n_agents))) {
+                vk::set_error("vk_diffuse_coupled: bad gather / count rows");
+                return VK_ERR_ARG;
+            }
+            cp.grow[f] = (int8_t)(gather_row[f] < 0 ? -1 : gather_row[f]);
+            cp.crow[f] = (int8_t)(count_row[f] < 0 ? -1 : count_row[f]);
+        }
+    }
+    // the plan: pair-sum passes only, at least two (the gather rides on the first,
+    // the exchange on the last)
+    int ks[64];
+    int np = 0;
+    const bool ten = g_stencil_depth == 10 && n_sub % 10 == 0 && n_sub >= 20;
+    if (g_stencil_mode != 1 || g_stencil_kernel < 20 || n_fields > VK_COUPLE_MAX_FIELDS || n_sub < 2) {
+        vk::set_error("vk_diffuse_coupled: needs the tolerance mode's pair-sum passes");
+        return VK_ERR_LIMIT;
+    }
+    if (ten) {
+        np = n_sub / 10;
+        if (np > 64) np = 0;
+        for (int p = 0; p < np; ++p) ks[p] = 10;
+    } else {
+        int depth = g_stencil_depth == 10 ? 9 : (g_stencil_depth | 1);
+        int passes = (n_sub + depth - 1) / depth;
+        if ((passes & 1) != (n_sub & 1)) ++passes;
+        for (int j = 0, left = passes; j < n_sub && np < 64; --left) {
+            const int rem = n_sub - j;
+            int k = (rem + left - 1) / left;
+            if ((k & 1) == 0) ++k;
+            if (k > depth) k = depth;
+            while (k > 1 && rem - k < left - 1) k -= 2;
+            ks[np++] = k;
+            j += k;
+        }
+        for (int p = 0; p < np; ++p)
+            if (ks[p] < 3 || ks[p] > 11) np = 0;
+    }
+    if (np < 2) {
+        vk::set_error("vk_diffuse_coupled: the step is not planned as two or more pair-sum passes");
+        return VK_ERR_LIMIT;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    // variants 26 / 27: one plane at a time (vk_diffuse)
+    const int nfl = g_stencil_kernel >= 26 ? 1 : n_fields;
+    for (int f = 0; f < n_fields; f += nfl) {
+        const int64_t off = (int64_t)f * field_stride;
+        double *pf = field + off, *w0 = work0 + off, *w1 = work1 + off;
+        VkPsCouple c = cp;
+        for (int i = 0; i < nfl; ++i) {
+            c.grow[i] = cp.grow[f + i];
+            c.crow[i] = cp.crow[f + i];
+        }
+        const double *cur = pf;
+        for (int p = 0, j = 0; p < np; j += ks[p], ++p) {
+            const bool last = p == np - 1;
+            double *dst;
+            if (last) dst = pf;
+            else if (ten) dst = cur == w0 ? w1 : w0;
+            else dst = (j + ks[p] - 1) & 1 ? w1 : w0;   // work[e & 1], e = this pass's last substep
+            c.mode = n_agents > 0 ? (p == 0 ? 1 : 0) | (last ? 2 : 0) : 0;
+            vk_launch_ps_alt(g_stencil_kernel, ks[p], s, cur, dst, nullptr, nfl, field_stride, ny, 0, rows, 0, rows,
+                             0, rows - 1, coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
+            const int rc = vk::launch_check("vk_diffuse_coupled kernel");
+            if (rc) return rc;
+            cur = dst;
+        }
     }
     return VK_OK;
 }

@@ -17,6 +17,27 @@ extern int g_stencil_stagger;  // pair-sum passes: odd tile columns' chunk grid 
 void vk_launch_wl3(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 3 rows prefetched
 void vk_launch_wl6(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 6 rows prefetched
 void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS);        // as wl6 with streaming stores (k = 7, 9, 11; 10 tolerance mode)
-void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS);           // tolerance mode, pair-sum form (k = 3, 5, 7, 9, 11)
-void vk_launch_ps10(VK_STENCIL_LAUNCH_ARGS);         // the same, k = 10
-void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS);   // variant 20-22 dispatch (21 / 22: A/B alternates)
+// Agent coupling carried by a pair-sum pass (vk_diffuse_coupled): each wave
+// handles the agents whose bins lie in its own output rows x columns.  Agents
+// are stored in bin order (bins ascending); seg[r * nseg + s] = the first agent
+// with bin >= r * ny + 16 s.
+#define VK_COUPLE_MAX_FIELDS 8
+struct VkPsCouple {
+    const int32_t *bins;
+    const int32_t *seg;
+    int32_t nseg;
+    int32_t n;                             // agents
+    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it
+    double *gdst;                          // gather: gdst[grow[f] * gld + a] = plane f at bins[a] (pre-pass)
+    int64_t gld;
+    const int64_t *counts;                 // exchange: plane f += counts[crow[f] * cld + a] / bva * 1000
+    int64_t cld;
+    double bva;
+    int8_t grow[VK_COUPLE_MAX_FIELDS];     // -1 = none
+    int8_t crow[VK_COUPLE_MAX_FIELDS];
+};
+
+void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS, const VkPsCouple *cp);     // tolerance mode, pair-sum form (k = 3, 5, 7, 9, 11)
+void vk_launch_ps10(VK_STENCIL_LAUNCH_ARGS, const VkPsCouple *cp);   // the same, k = 10
+// variant 20-25 dispatch (21-25: A/B alternates); cp (nullable) = agent coupling
+void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS, const VkPsCouple *cp = nullptr);

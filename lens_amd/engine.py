@@ -109,7 +109,9 @@ class Experiment:
         self.dividers: Dict[Tuple, object] = {}   # store path (with '*' globs) -> schema _divider
         self._div_globs: List[Tuple] = []
         self._structure = 0                        # moves when processes join or leave the tree
-        self._deleted = set()                      # ids of processes deleted from the tree
+        # processes deleted from the tree during the current send_updates, by id -- the
+        # objects are held so that no new process can reuse a deleted one's id
+        self._deleted = {}
         self._state_seen = None
         self.local_time = 0.0
         for path, proc in self._walk(self.processes, ()):
@@ -352,7 +354,7 @@ class Experiment:
         if isinstance(pnode, dict) and path[-1] in pnode:
             lost = pnode.pop(path[-1])
             for _, proc in (self._walk(lost, ()) if isinstance(lost, dict) else [((), lost)]):
-                self._deleted.add(id(proc))
+                self._deleted[id(proc)] = proc
                 self._ports.pop(id(proc), None)
         self._structure_changed()
 
@@ -476,6 +478,7 @@ class Experiment:
             self._version += 1
 
     def send_updates(self, updates, derivers=None):
+        self._deleted = {}
         for update, path in updates:
             raw = getattr(update, 'raw', None)
             if raw is not None:

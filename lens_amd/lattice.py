@@ -16,6 +16,7 @@ for a persistent SoA colony:
 
 from __future__ import annotations
 
+import ctypes
 from typing import Callable, Optional, Sequence
 
 import torch
@@ -207,6 +208,68 @@ class Lattice:
             events[1].record()
         return n_sub
 
+    def coupled_plan_ok(self, timestep: float) -> bool:
+        """Whether :meth:`diffuse_coupled` can run this step: a whole plane (no
+        row band) planned as two or more pair-sum passes -- the tolerance mode
+        with kernel variants 20-25 and pass depths 3..11 (vk_diffuse's planner,
+        restated; vk_diffuse_coupled makes the same decision and launches
+        nothing otherwise)."""
+        if self.pad_top or self.pad_bot or not (self.edge_top and self.edge_bot) or len(self.molecules) > 8:
+            return False
+        if native._lib.vk_set_stencil_mode(-1) != 1 or native._lib.vk_set_stencil_kernel(-1, -1) < 20:
+            return False
+        n_sub = n_substeps(timestep, self.diffusion_dt)
+        depth = native._lib.vk_set_stencil_depth(0)
+        if depth == 10 and n_sub % 10 == 0 and n_sub >= 20:
+            return True
+        depth = 9 if depth == 10 else depth | 1
+        passes = (n_sub + depth - 1) // depth
+        if (passes & 1) != (n_sub & 1):
+            passes += 1
+        ks, j, left = [], 0, passes
+        while j < n_sub:
+            rem = n_sub - j
+            k = (rem + left - 1) // left
+            k += 1 - (k & 1)
+            k = min(k, depth)
+            while k > 1 and rem - k < left - 1:
+                k -= 2
+            ks.append(k)
+            j += k
+            left -= 1
+        return len(ks) >= 2 and all(3 <= k <= 11 for k in ks)
+
+    def diffuse_coupled(self, timestep: float, bin_lin, n_agents: int, seg, gather_rows, conc, count_rows,
+                        counts, allreduce: Optional[Callable] = None, events=None):
+        """One whole-plane step (:meth:`diffuse`) whose first pass also gathers
+        the agents' external concentrations from the pre-step planes
+        (:meth:`gather`) and whose final pass also scatters the exchange counts
+        into the new planes (:meth:`exchange_sorted`), with the same results
+        (vk_diffuse_coupled).  The agents must be stored in bin order; ``seg``
+        indexes them by 16-column segment (:func:`segment_index`).
+        ``gather_rows`` / ``count_rows``: per plane, the SoA row it gathers
+        into / takes its counts from (-1: none).  Check :meth:`coupled_plan_ok`
+        first; returns False, having launched only the uniform probe, if the
+        library declines the plan."""
+        n_sub = n_substeps(timestep, self.diffusion_dt)
+        coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
+        mm = self.uniform_summary(allreduce)
+        if events is not None:
+            events[0].record()
+        nf = len(self.molecules)
+        rc = native._lib.vk_diffuse_coupled(
+            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1), nf, self.field_stride,
+            self.ny, self.rows_local, n_sub, coeff_dt, native.ptr(mm), native.ptr(bin_lin), native.ptr(seg),
+            (self.ny + 15) // 16, int(n_agents), (ctypes.c_int32 * nf)(*gather_rows), native.ptr(conc),
+            conc.shape[1], (ctypes.c_int32 * nf)(*count_rows), native.ptr(counts), counts.shape[1],
+            self.binvol_avogadro, native.stream_handle())
+        if rc == native.VK_ERR_LIMIT:
+            return False
+        native.check(rc, 'vk_diffuse_coupled')
+        if events is not None:
+            events[1].record()
+        return True
+
     def exchange_first_halo(self, timestep: float, halo_exchange: Callable, stream):
         """Run the halo exchange of :meth:`diffuse`'s first block on ``stream``
         (a communication stream), so it overlaps what the launch stream does
@@ -302,6 +365,17 @@ class Lattice:
             native.ptr(counts), counts.shape[1], native.ptr(map_count), native.ptr(map_field),
             int(map_count.numel()), self.binvol_avogadro, native.stream_handle()),
             'vk_exchange_atomic')
+
+
+def segment_index(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int) -> torch.Tensor:
+    """For agents stored in bin order: seg[r * nseg + s] = the first agent whose
+    bin is >= r * ny + 16 s (nseg = ceil(ny / 16)), the index the coupled
+    passes find a row segment's agents with (vk_diffuse_coupled)."""
+    nseg = (ny + 15) // 16
+    dev = bin_lin.device
+    targets = (torch.arange(rows, dtype=torch.int64, device=dev)[:, None] * ny +
+               16 * torch.arange(nseg, dtype=torch.int64, device=dev)[None, :]).reshape(-1)
+    return torch.searchsorted(bin_lin[:n_agents].to(torch.int64), targets).to(torch.int32)
 
 
 def occupancy(bin_lin: torch.Tensor, n_agents: int, order_key: Optional[torch.Tensor] = None):

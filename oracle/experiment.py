@@ -130,7 +130,7 @@ class OracleExperiment:
         self.schema = {}                      # store path (with '*' globs) -> updater name
         self._globs = []                      # the schema paths holding a '*'
         self.dividers = {}                    # store path (with '*' globs) -> _divider
-        self.deleted = set()                  # ids of processes removed from the tree
+        self.deleted = {}                     # processes removed during the current pass, by id (held)
         self.local_time = 0.0
         for path, proc in self._walk(processes, ()):
             for port, port_schema in proc.ports_schema().items():
@@ -286,7 +286,7 @@ class OracleExperiment:
         if path[-1] in pnode:
             lost = pnode.pop(path[-1])
             for _, proc in (self._walk(lost, ()) if isinstance(lost, dict) else [((), lost)]):
-                self.deleted.add(id(proc))
+                self.deleted[id(proc)] = proc      # held: a new process must not reuse the id
 
     def divider_at(self, path):
         if path in self.dividers:
@@ -314,6 +314,7 @@ class OracleExperiment:
         return None
 
     def send_updates(self, updates, derivers=None):
+        self.deleted = {}                      # processes deleted during this pass
         for update, path in updates:
             self.apply_update(update, path)
         if derivers is None:
@@ -409,8 +410,14 @@ class OracleConvenienceKinetics(OracleProcess):
         for port, states in self.initial_state.items():
             for k, v in states.items():
                 schema[port][k] = {'_default': v}
+        schema['fields'] = {k: {'_default': np.ones((1, 1))} for k in schema['external']}
         for rid in self.agent.model.reaction_ids:
             schema['fluxes'][rid] = {'_default': 0.0, '_updater': 'set'}
+        # convenience_kinetics.py:269-285: declared, so a daughter's store holds them
+        # (no divider: each daughter keeps the mother's value)
+        schema['global'] = {'mmol_to_counts': {'_default': 0.0}, 'location': {'_default': [0.5, 0.5]}}
+        schema['dimensions'] = {'bounds': {'_default': [1, 1]}, 'n_bins': {'_default': [1, 1]},
+                                'depth': {'_default': 1}}
         return schema
 
     def next_update(self, timestep, states):

@@ -176,3 +176,25 @@ def test_generate_delete_add_updates(structure):
     a, b = snaps('engine'), snaps('oracle')
     assert a == b
     assert len(a[-1][0]) == {'generate': 6, 'delete': 0, 'add': 6}[structure]
+
+
+def test_deleted_derivers_are_forgotten_after_their_pass():
+    """A deriver deleted in one send_updates pass is skipped only in that pass:
+    the ids of deleted processes must not outlive it, or a new process that
+    reuses a freed object's id would never run (the engine and the oracle hold
+    the deleted objects for the pass and start every pass afresh)."""
+    for kind in ('engine', 'oracle'):
+        np.random.seed(0)
+        random.seed(0)
+        p, t, init = colony(2)
+        exp = Experiment({'processes': p, 'topology': t, 'initial_state': init}) if kind == 'engine' else \
+            OracleExperiment(p, t, init)
+        deriver = exp.processes['agents']['0']['division']
+        stale = {id(deriver): deriver}
+        if kind == 'engine':
+            exp._deleted = stale
+        else:
+            exp.deleted = stale
+        exp.state['agents']['0']['boundary']['divide'] = True
+        exp.send_updates([])
+        assert '0' not in exp.state['agents'] and '00' in exp.state['agents'], kind

@@ -86,6 +86,15 @@ def _to_host(x):
     return x
 
 
+def _host_tree(t):
+    if isinstance(t, dict):
+        return {k: _host_tree(v) for k, v in t.items()}
+    if isinstance(t, list):
+        return [_host_tree(v) for v in t]
+    x = _to_host(t)
+    return x.copy() if isinstance(x, np.ndarray) else x
+
+
 def _compare(a, b, path=()):
     if isinstance(b, dict):
         assert isinstance(a, dict) and sorted(a) == sorted(b), path
@@ -317,8 +326,8 @@ def test_dividing_colony_through_batched_loop_equals_reference_restatement():
             if batched:
                 torch.cuda.synchronize()
             fields = {m: _to_host(v).copy() for m, v in exp.state['fields'].items()}
-            agents = {k: {port: dict(v) if isinstance(v, dict) else v for port, v in st.items()}
-                      for k, st in exp.state['agents'].items()}
+            # a deep copy: a loop may update nested stores (boundary.external) in place
+            agents = _host_tree(exp.state['agents'])
             out.append((exp.local_time, list(exp.state['agents']), agents, fields,
                         sorted(exp.processes['agents'])))
         return out
