@@ -195,42 +195,58 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
     const int bot_reflect = edge_bot ? hi_max - 1 : 0x7fffffff;
     hipStream_t s = (hipStream_t)stream;
     const int last_in_call = sub_begin + sub_count - 1;
-    if (g_stencil_depth == 10 && g_stencil_mode == 1 && sub_begin == 0 && sub_count == n_sub && n_sub % 10 == 0 &&
-        n_sub >= 20 && work1) {
-        // Tolerance mode, whole step, 10 k substeps: k passes of 10.  The final pass
-        // writes the field without reading it back (no f0), so the field is a third
-        // buffer: pass p reads `cur` and writes the work buffer it did not read, and the
-        // last pass writes the field.  Uniform planes skip every pass and keep their field.
-        // variants 26 / 27: one plane at a time, its passes back to back
-        const int nfl = g_stencil_kernel >= 26 ? 1 : n_fields;
-        for (int f = 0; f < n_fields; f += nfl) {
-            const int64_t off = (int64_t)f * field_stride;
-            double *pf = field + off, *w0 = work0 + off, *w1 = work1 + off;
-            const double *cur = pf;
-            for (int j = 0, p = 0; j < n_sub; j += 10, ++p) {
-                const int e = j + 9;
-                const int grow = last_in_call - e;
-                const int lo = max(lo_min, row_lo - grow);
-                const int hi = min(hi_max, row_hi + grow);
-                const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
-                double *dst = (e == n_sub - 1) ? pf : (cur == w0 ? w1 : w0);
-                launch_fast10(s, cur, dst, nfl, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
-                              coeff_dt, uniform ? uniform + 2 * f : nullptr);
-                int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
-                if (rc) return rc;
-                cur = dst;
+    if (g_stencil_depth == 10 && g_stencil_mode == 1 && sub_count % 10 == 0 && work1) {
+        // Tolerance mode, a block of 10 k substeps: k passes of 10.  The final pass
+        // writes the field without reading it back (no f0), so when the block ends the
+        // step the field is a third buffer (its step-start values are not needed once
+        // the first pass has read them).  The block starts in the buffer the odd-depth
+        // convention holds the state in (field for substep 0, else work[(j-1)&1]) and
+        // ends in the one it expects after the block (field after the last substep,
+        // else work[last & 1]), so halo exchanges between blocks (row bands) see the
+        // usual buffers.  Buffers are assigned backwards from the target: each pass
+        // writes one its source is not.  Uniform planes skip every pass (nothing reads
+        // the buffers they leave unwritten) and keep their field.
+        const int P = sub_count / 10;
+        const bool ends_step = last_in_call == n_sub - 1;
+        double *S = sub_begin == 0 ? field : work[(sub_begin - 1) & 1];
+        double *T = ends_step ? field : work[last_in_call & 1];
+        double *cand[3] = {work0, work1, field};
+        const int nc = ends_step ? 3 : 2;    // the field is scratch only in a block that ends the step
+        double *dsts[64];
+        bool ok = P >= 1 && P <= 64;
+        for (int p = P - 1; ok && p >= 0; --p) {
+            if (p == P - 1) {
+                dsts[p] = T;
+            } else {
+                dsts[p] = nullptr;
+                for (int c = 0; c < nc && !dsts[p]; ++c)
+                    if (cand[c] != dsts[p + 1] && (p > 0 || cand[c] != S)) dsts[p] = cand[c];
+                ok = dsts[p] != nullptr;
             }
         }
-        return VK_OK;
-    }
-    if (g_stencil_depth == 10 && g_stencil_mode == 1 && sub_begin == 0 && sub_count == 10 && n_sub > 10) {
-        // one 10-deep pass from the field into work1 (the buffer the odd-depth plans'
-        // convention gives the state after substep 9): the bench's single-pass timing
-        const int grow = last_in_call - 9;
-        const int lo = max(lo_min, row_lo - grow), hi = min(hi_max, row_hi + grow);
-        launch_fast10(s, field, work1, n_fields, field_stride, ny, lo, hi, max(lo_min, lo - 10),
-                      min(hi_max, hi + 10), top_reflect, bot_reflect, coeff_dt, uniform);
-        return vk::launch_check("vk_diffuse kernel (depth 10)");
+        ok = ok && dsts[0] != S;
+        if (ok) {
+            // variants 26 / 27: one plane at a time, its passes back to back
+            const int nfl = g_stencil_kernel >= 26 ? 1 : n_fields;
+            for (int f = 0; f < n_fields; f += nfl) {
+                const int64_t off = (int64_t)f * field_stride;
+                const double *cur = S + off;
+                for (int p = 0; p < P; ++p) {
+                    const int e = sub_begin + 10 * p + 9;
+                    const int grow = last_in_call - e;
+                    const int lo = max(lo_min, row_lo - grow);
+                    const int hi = min(hi_max, row_hi + grow);
+                    const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
+                    double *dst = dsts[p] + off;
+                    launch_fast10(s, cur, dst, nfl, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
+                                  coeff_dt, uniform ? uniform + 2 * f : nullptr);
+                    int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
+                    if (rc) return rc;
+                    cur = dst;
+                }
+            }
+            return VK_OK;
+        }
     }
     int depth = g_stencil_depth | 1;   // odd
     if (g_stencil_depth == 10) depth = 9;

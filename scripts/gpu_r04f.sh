@@ -9,4 +9,6 @@ timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method threa
 tail -2 $O/pytest_coupled.log
 timeout -k 10 300 python -u scripts/stencil_sweep.py 4096 20:10:34:1,23:10:34:1,24:10:34:1,25:10:34:1,26:10:34:1,27:10:34:1,26:10:17:1,26:10:26:1,26:10:51:1,23:10:40:1 > $O/sweep.log 2>&1 || { tail -20 $O/sweep.log; exit 5; }
 cat $O/sweep.log
+timeout -k 10 300 python -u scripts/rank_emulate.py 8 --sweep 100:16:20:10,50:16:20:10,50:24:20:10,20:16:20:10,20:24:20:10,100:24:20:10,100:12:20:10,30:16:20:10 > $O/rank_sweep.log 2>&1 || { tail -20 $O/rank_sweep.log; exit 7; }
+cat $O/rank_sweep.log
 TAG=r04f bash scripts/gpu_full.sh || exit $?

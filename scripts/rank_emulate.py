@@ -3,22 +3,23 @@
 substeps, each block preceded by a local stand-in for the halo exchange (the
 same 4 row-copies per field the real exchange does; no RCCL).  The whole plane is
 timed live in the same process with the settings the one-GPU bench uses (34-row
-tiles), and the band is reported against 1/N of it.  Prints ms per step.
+tiles, variant 20, depth 10, tolerance mode), and each band is reported against
+1/N of it.  Prints ms per step.
 
     python scripts/rank_emulate.py N halo rows [variant depth [mode]]     (mode: exact | fma)
+    python scripts/rank_emulate.py N --sweep halo:rows:variant:depth,...  (tolerance mode)
 """
-import os, sys, time
+import json
+import os
+import sys
+import time
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch
-from lens_amd import configs
-from lens_amd.lattice import Lattice, stencil_depth, stencil_kernel
-from lens_amd.distributed import row_bands
-world, halo, rows = (int(x) for x in sys.argv[1:4])
-variant = int(sys.argv[4]) if len(sys.argv) > 4 else 20
-depth = int(sys.argv[5]) if len(sys.argv) > 5 else 10
-mode = sys.argv[6] if len(sys.argv) > 6 else 'fma'
-from lens_amd.lattice import stencil_mode
-stencil_mode(mode)
+import torch  # noqa: E402
+from lens_amd import configs  # noqa: E402
+from lens_amd.distributed import row_bands  # noqa: E402
+from lens_amd.lattice import Lattice, stencil_depth, stencil_kernel, stencil_mode  # noqa: E402
+
 dev = torch.device('cuda', 0)
 nx = 4096
 
@@ -34,31 +35,65 @@ def time_steps(fn, warm=20, reps=10):
     return (time.perf_counter() - t0) / reps * 1e3
 
 
-glc0 = configs.gaussian_bump_field((nx, nx))
-whole = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev,
-                initial={'glc__D_e': glc0, 'ac_e': glc0 * 0.5})
-stencil_kernel(variant, 34)
-stencil_depth(depth)
-whole_ms = time_steps(lambda: whole.diffuse(1.0))
-del whole
-band = row_bands(nx, world)[1 if world > 2 else 0]
-glc = configs.gaussian_bump_field((nx, nx))
-lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev, row_band=band,
-              halo=halo, initial={'glc__D_e': glc, 'ac_e': glc * 0.5})
-stencil_kernel(variant, rows)
-stencil_depth(depth)
-h = lat.halo
-bufs = [torch.empty((2, h, nx), dtype=torch.float64, device=dev) for _ in range(4)]
+def whole_plane_ms(variant=20, depth=10, rows=34):
+    glc0 = configs.gaussian_bump_field((nx, nx))
+    whole = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev,
+                    initial={'glc__D_e': glc0, 'ac_e': glc0 * 0.5})
+    stencil_kernel(variant, rows)
+    stencil_depth(depth)
+    ms = time_steps(lambda: whole.diffuse(1.0))
+    del whole
+    return ms
 
-def fake_exchange(src, cnt):
-    if not lat.edge_top:
-        bufs[0].copy_(src[:, lat.row_lo:lat.row_lo + h]); bufs[1].copy_(bufs[0])
-        src[:, lat.row_lo - h:lat.row_lo].copy_(bufs[1])
-    if not lat.edge_bot:
-        bufs[2].copy_(src[:, lat.row_hi - h:lat.row_hi]); bufs[3].copy_(bufs[2])
-        src[:, lat.row_hi:lat.row_hi + h].copy_(bufs[3])
 
-ms = time_steps(lambda: lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None))
-print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step; whole plane %.3f ms (live), '
-      'ideal %.3f = 1/N of it, diffusion efficiency %.2f' % (world, band, halo, rows, variant, depth, mode, ms,
-                                                             whole_ms, whole_ms / world, whole_ms / world / ms))
+def band_ms(world, halo, rows, variant, depth):
+    band = row_bands(nx, world)[1 if world > 2 else 0]
+    glc = configs.gaussian_bump_field((nx, nx))
+    lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev, row_band=band,
+                  halo=halo, initial={'glc__D_e': glc, 'ac_e': glc * 0.5})
+    stencil_kernel(variant, rows)
+    stencil_depth(depth)
+    h = lat.halo
+    bufs = [torch.empty((2, h, nx), dtype=torch.float64, device=dev) for _ in range(4)]
+
+    def fake_exchange(src, cnt):
+        if not lat.edge_top:
+            bufs[0].copy_(src[:, lat.row_lo:lat.row_lo + h]); bufs[1].copy_(bufs[0])
+            src[:, lat.row_lo - h:lat.row_lo].copy_(bufs[1])
+        if not lat.edge_bot:
+            bufs[2].copy_(src[:, lat.row_hi - h:lat.row_hi]); bufs[3].copy_(bufs[2])
+            src[:, lat.row_hi:lat.row_hi + h].copy_(bufs[3])
+
+    ms = time_steps(lambda: lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None))
+    del lat
+    return band, ms
+
+
+def main():
+    world = int(sys.argv[1])
+    if len(sys.argv) > 2 and sys.argv[2] == '--sweep':
+        stencil_mode('fma')
+        whole = whole_plane_ms()
+        print(json.dumps({'world': world, 'whole_plane_ms': round(whole, 4), 'ideal_ms': round(whole / world, 4)}),
+              flush=True)
+        for spec in sys.argv[3].split(','):
+            halo, rows, variant, depth = (int(x) for x in spec.split(':'))
+            band, ms = band_ms(world, halo, rows, variant, depth)
+            print(json.dumps({'world': world, 'band': list(band), 'halo': halo, 'rows': rows, 'variant': variant,
+                              'depth': depth, 'ms_per_step': round(ms, 4),
+                              'efficiency': round(whole / world / ms, 3)}), flush=True)
+        return
+    halo, rows = int(sys.argv[2]), int(sys.argv[3])
+    variant = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    depth = int(sys.argv[5]) if len(sys.argv) > 5 else 10
+    mode = sys.argv[6] if len(sys.argv) > 6 else 'fma'
+    stencil_mode(mode)
+    whole = whole_plane_ms()
+    band, ms = band_ms(world, halo, rows, variant, depth)
+    print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step; whole plane %.3f ms (live), '
+          'ideal %.3f = 1/N of it, diffusion efficiency %.2f' % (world, band, halo, rows, variant, depth, mode, ms,
+                                                                 whole, whole / world, whole / world / ms))
+
+
+if __name__ == '__main__':
+    main()

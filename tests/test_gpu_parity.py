@@ -549,6 +549,34 @@ def test_banded_depth10_plan_equals_whole(dev):
                     int(lat.edge_bot), 0, 100, 100, lat.diffusion * 0.01, 0, native.stream_handle()), 'diffuse')
             got = torch.cat([lat.owned('a') for lat in lats], 0).cpu().numpy()
             assert np.array_equal(got, whole.owned('a').cpu().numpy()), world
+        # shallower halos: blocks of 10 k substeps are 10-deep passes too, chained
+        # through the buffers the halo exchanges read (work[(j-1)&1] before block j)
+        for world, halo in ((3, 50), (3, 20), (2, 30)):
+            bands = row_bands(nx, world)
+            lats = [Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                            row_band=b, halo=halo, initial={'a': f0}) for b in bands]
+            j = 0
+            while j < 100:
+                cnt = min(halo, 100 - j)
+                name = 'fields' if j == 0 else ('work0' if ((j - 1) & 1) == 0 else 'work1')
+                for r, lat in enumerate(lats):
+                    src = getattr(lat, name)
+                    if not lat.edge_top:
+                        nb = getattr(lats[r - 1], name)
+                        src[:, lat.row_lo - halo:lat.row_lo].copy_(nb[:, lats[r - 1].row_hi - halo:lats[r - 1].row_hi])
+                    if not lat.edge_bot:
+                        nb = getattr(lats[r + 1], name)
+                        src[:, lat.row_hi:lat.row_hi + halo].copy_(nb[:, lats[r + 1].row_lo:lats[r + 1].row_lo + halo])
+                for lat in lats:
+                    lo_min = lat.row_lo if lat.edge_top else 0
+                    hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
+                    native.check(native._lib.vk_diffuse(
+                        native.ptr(lat.fields), native.ptr(lat.work0), native.ptr(lat.work1), 1,
+                        lat.field_stride, ny, lat.row_lo, lat.row_hi, lo_min, hi_max, int(lat.edge_top),
+                        int(lat.edge_bot), j, cnt, 100, lat.diffusion * 0.01, 0, native.stream_handle()), 'diffuse')
+                j += cnt
+            got = torch.cat([lat.owned('a') for lat in lats], 0).cpu().numpy()
+            assert np.array_equal(got, whole.owned('a').cpu().numpy()), (world, halo)
     finally:
         stencil_mode(prev_m)
         stencil_depth(prev_d)
