@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <utility>
+#include <vector>
 
 
 #include "vk_internal.h"
@@ -160,15 +161,49 @@ __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ sr
         dst[base + i] = src[base + i];
 }
 
-// One tolerance-mode 10-deep pass (no base plane): pair-sum passes, or the
-// variant-6 FMA form when that variant is selected
-static void launch_fast10(hipStream_t s, const double *src, double *dst, int nf, int64_t fs, int ny, int lo, int hi,
-                          int in_lo, int in_hi, int top, int bot, double coef, const double *mm) {
-    if (g_stencil_kernel >= 20)
-        vk_launch_ps_alt(g_stencil_kernel, 10, s, src, dst, nullptr, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef,
-                         mm);
-    else
-        vk_launch_wl6nt(10, s, src, dst, nullptr, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm);
+// One fused pass of k >= 2 substeps, the kernel picked by mode / variant / depth;
+// f0 != nullptr marks the exact mode's final pass (it re-reads the step-start plane).
+// cp (nullable): the agent coupling the pass carries (vk_diffuse_coupled).
+static void launch_pass(int k, hipStream_t s, const double *src, double *dst, const double *f0, int nf, int64_t fs,
+                        int ny, int lo, int hi, int in_lo, int in_hi, int top, int bot, double coef, const double *mm,
+                        const VkPsCouple *cp) {
+    if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11) {
+        // tolerance mode, pair-sum passes (the final pass writes the new field as is)
+        vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+    } else if (k == 10 ||
+               ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11))) {
+        // variant 6 (streaming stores); k = 10 is the tolerance mode's 4-op FMA form
+        vk_launch_wl6nt(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+    } else {
+        // other depths (and variants 2 / 3): the plain-store wave tiles; the final pass
+        // also streams the base plane (3 rows ahead), so it keeps the shallow row
+        // prefetch and still fits 3 waves per SIMD
+        auto launch = (g_stencil_kernel == 2 || f0) ? vk_launch_wl3 : vk_launch_wl6;
+        launch(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+    }
+}
+
+// The odd-depth pass plan of a call's substeps [sub_begin, last]: the fewest odd
+// depths <= the set depth that sum to the count (a sum of P odd numbers has the
+// parity of P), as even as possible -- e.g. 100 = 8x9 + 4x7 rather than 11x9 + a
+// lone single-substep pass.
+static std::vector<int> odd_plan(int sub_count) {
+    int depth = g_stencil_depth | 1;   // odd
+    if (g_stencil_depth == 10) depth = 9;
+    if (depth > 15) depth = 15;
+    int passes = (sub_count + depth - 1) / depth;
+    if ((passes & 1) != (sub_count & 1)) ++passes;
+    std::vector<int> ks;
+    for (int j = 0, left = passes; j < sub_count; --left) {
+        const int rem = sub_count - j;   // rem has the parity of `left`
+        int k = (rem + left - 1) / left;
+        if ((k & 1) == 0) ++k;
+        if (k > depth) k = depth;
+        while (k > 1 && rem - k < left - 1) k -= 2;
+        ks.push_back(k);
+        j += k;
+    }
+    return ks;
 }
 
 extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
@@ -204,7 +239,9 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         // ends in the one it expects after the block (field after the last substep,
         // else work[last & 1]), so halo exchanges between blocks (row bands) see the
         // usual buffers.  Buffers are assigned backwards from the target: each pass
-        // writes one its source is not.  Uniform planes skip every pass (nothing reads
+        // writes one its source is not (a block inside the step starts and ends in the
+        // same work buffer, so it needs an even number of passes; otherwise it takes
+        // the odd-depth plan below).  Uniform planes skip every pass (nothing reads
         // the buffers they leave unwritten) and keep their field.
         const int P = sub_count / 10;
         const bool ends_step = last_in_call == n_sub - 1;
@@ -238,8 +275,8 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
                     const int hi = min(hi_max, row_hi + grow);
                     const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
                     double *dst = dsts[p] + off;
-                    launch_fast10(s, cur, dst, nfl, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
-                                  coeff_dt, uniform ? uniform + 2 * f : nullptr);
+                    launch_pass(10, s, cur, dst, nullptr, nfl, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
+                                bot_reflect, coeff_dt, uniform ? uniform + 2 * f : nullptr, nullptr);
                     int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
                     if (rc) return rc;
                     cur = dst;
@@ -248,20 +285,10 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             return VK_OK;
         }
     }
-    int depth = g_stencil_depth | 1;   // odd
-    if (g_stencil_depth == 10) depth = 9;
-    if (depth > 15) depth = 15;
-    // Pass plan: the fewest odd depths <= depth that sum to sub_count (a sum of
-    // P odd numbers has the parity of P), as even as possible -- e.g. 100 =
-    // 8x9 + 4x7 rather than 11x9 + a lone single-substep pass.
-    int passes = (sub_count + depth - 1) / depth;
-    if ((passes & 1) != (sub_count & 1)) ++passes;
-    for (int j = sub_begin, left = passes; j <= last_in_call; --left) {
-        const int rem = last_in_call - j + 1;   // rem has the parity of `left`
-        int k = (rem + left - 1) / left;
-        if ((k & 1) == 0) ++k;
-        if (k > depth) k = depth;
-        while (k > 1 && rem - k < left - 1) k -= 2;
+    const std::vector<int> ks = odd_plan(sub_count);
+    int j = sub_begin;
+    for (size_t p = 0; p < ks.size(); ++p) {
+        const int k = ks[p];
         const int e = j + k - 1;     // last substep of this pass
         const int grow = last_in_call - e;
         const int lo = max(lo_min, row_lo - grow);
@@ -278,21 +305,9 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
             dim3 grid((ny + ST_BX - 1) / ST_BX, (hi - lo + ST_RB - 1) / ST_RB, n_fields);
             hipLaunchKernelGGL(k_diffuse_substep, grid, dim3(ST_BX), 0, s, src, dst, f0, field_stride, ny, lo,
                                hi, top_reflect, bot_reflect, coeff_dt, uniform, 0);
-        } else if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11) {
-            // tolerance mode, pair-sum passes (the final pass writes the new field as is)
-            vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi,
-                             top_reflect, bot_reflect, coeff_dt, uniform);
-        } else if ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) &&
-                   (k == 7 || k == 9 || k == 11)) {
-            vk_launch_wl6nt(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
-                            bot_reflect, coeff_dt, uniform);
         } else {
-            // other depths (and variants 2 / 3): the plain-store wave tiles; the final pass
-            // also streams the base plane (3 rows ahead), so it keeps the shallow row
-            // prefetch and still fits 3 waves per SIMD
-            auto launch = (g_stencil_kernel == 2 || f0) ? vk_launch_wl3 : vk_launch_wl6;
-            launch(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
-                   coeff_dt, uniform);
+            launch_pass(k, s, src, dst, f0, n_fields, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect, bot_reflect,
+                        coeff_dt, uniform, nullptr);
         }
         int rc = vk::launch_check("vk_diffuse kernel");
         if (rc) return rc;
@@ -313,8 +328,9 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
 // pass also gathers each agent's external concentrations from the pre-step
 // planes, the final pass also scatters the exchange into the new planes (one
 // launch each less, and the exchange's read-modify-write of the planes happens
-// while the final pass holds them).  Returns VK_ERR_LIMIT, launching nothing,
-// when the step is not planned as two or more pair-sum passes.
+// while the final pass holds them).  Either arithmetic mode.  Returns
+// VK_ERR_LIMIT, launching nothing, when the step is not planned as two or more
+// fused passes.
 extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fields,
                                   int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
                                   const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
@@ -349,42 +365,25 @@ extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, i
             cp.crow[f] = (int8_t)(count_row[f] < 0 ? -1 : count_row[f]);
         }
     }
-    // the plan: pair-sum passes only, at least two (the gather rides on the first,
-    // the exchange on the last)
-    int ks[64];
-    int np = 0;
-    const bool ten = g_stencil_depth == 10 && n_sub % 10 == 0 && n_sub >= 20;
-    if (g_stencil_mode != 1 || g_stencil_kernel < 20 || n_fields > VK_COUPLE_MAX_FIELDS || n_sub < 2) {
-        vk::set_error("vk_diffuse_coupled: needs the tolerance mode's pair-sum passes");
+    // the plan: vk_diffuse's (10-deep passes in the tolerance mode's depth-10 setting,
+    // else odd depths), at least two fused passes (the gather rides on the first, the
+    // exchange on the last) and no single-substep pass
+    if (n_fields > VK_COUPLE_MAX_FIELDS || n_sub < 2) {
+        vk::set_error("vk_diffuse_coupled: at most 8 planes and 2 substeps");
         return VK_ERR_LIMIT;
     }
-    if (ten) {
-        np = n_sub / 10;
-        if (np > 64) np = 0;
-        for (int p = 0; p < np; ++p) ks[p] = 10;
-    } else {
-        int depth = g_stencil_depth == 10 ? 9 : (g_stencil_depth | 1);
-        int passes = (n_sub + depth - 1) / depth;
-        if ((passes & 1) != (n_sub & 1)) ++passes;
-        for (int j = 0, left = passes; j < n_sub && np < 64; --left) {
-            const int rem = n_sub - j;
-            int k = (rem + left - 1) / left;
-            if ((k & 1) == 0) ++k;
-            if (k > depth) k = depth;
-            while (k > 1 && rem - k < left - 1) k -= 2;
-            ks[np++] = k;
-            j += k;
-        }
-        for (int p = 0; p < np; ++p)
-            if (ks[p] < 3 || ks[p] > 11) np = 0;
-    }
-    if (np < 2) {
-        vk::set_error("vk_diffuse_coupled: the step is not planned as two or more pair-sum passes");
+    const bool ten = g_stencil_depth == 10 && g_stencil_mode == 1 && n_sub % 10 == 0 && n_sub >= 20;
+    std::vector<int> ks = ten ? std::vector<int>(n_sub / 10, 10) : odd_plan(n_sub);
+    bool ok = ks.size() >= 2;
+    for (int k : ks) ok = ok && k >= 2;
+    if (!ok) {
+        vk::set_error("vk_diffuse_coupled: the step is not planned as two or more fused passes");
         return VK_ERR_LIMIT;
     }
     hipStream_t s = (hipStream_t)stream;
+    const int np = (int)ks.size();
     // variants 26 / 27: one plane at a time (vk_diffuse)
-    const int nfl = g_stencil_kernel >= 26 ? 1 : n_fields;
+    const int nfl = g_stencil_mode == 1 && g_stencil_kernel >= 26 ? 1 : n_fields;
     for (int f = 0; f < n_fields; f += nfl) {
         const int64_t off = (int64_t)f * field_stride;
         double *pf = field + off, *w0 = work0 + off, *w1 = work1 + off;
@@ -401,8 +400,9 @@ extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, i
             else if (ten) dst = cur == w0 ? w1 : w0;
             else dst = (j + ks[p] - 1) & 1 ? w1 : w0;   // work[e & 1], e = this pass's last substep
             c.mode = n_agents > 0 ? (p == 0 ? 1 : 0) | (last ? 2 : 0) : 0;
-            vk_launch_ps_alt(g_stencil_kernel, ks[p], s, cur, dst, nullptr, nfl, field_stride, ny, 0, rows, 0, rows,
-                             0, rows - 1, coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
+            // the exact mode's final pass re-reads the step-start plane: vk_diffuse's f0
+            launch_pass(ks[p], s, cur, dst, last ? pf : nullptr, nfl, field_stride, ny, 0, rows, 0, rows, 0, rows - 1,
+                        coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
             const int rc = vk::launch_check("vk_diffuse_coupled kernel");
             if (rc) return rc;
             cur = dst;

@@ -228,29 +228,13 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
                                               c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4);
 }
 
-// FAST = tolerance mode (vk_set_stencil_mode(1)): FMA-contracted arithmetic and a
-// final pass without the base re-read; within ~1e-14 relative of the exact mode.
-template <int K, int PD, bool FINAL, bool FAST = false>
-__device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *dst,
-                                                const double *f0, int64_t field_stride, int ny,
-                                                int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
-                                                int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
-                                                int n_fields, double coef, const double *__restrict__ uniform) {
+// The stencil work of one wave: its tile of plane f, output rows [c0, c1)
+template <int K, int PD, bool FINAL, bool FAST>
+__device__ __forceinline__ void diffuse_wl_tile_body(const double *__restrict__ src, double *dst, const double *f0,
+                                                     int64_t field_stride, int ny, int in_lo, int in_hi,
+                                                     int top_reflect, int bot_reflect, double coef, int f, int x0,
+                                                     int c0, int c1, int lane) {
     constexpr int KH = K + (K & 1);
-    constexpr int W = WT_COLS - 2 * KH;
-    // (An XCD-contiguous tile order -- each XCD's L2 serving its tiles' shared
-    // halo columns -- measured 4 % slower on 4096^2: the halo re-reads already
-    // hit the die-level Infinity Cache, so plain round-robin order is kept.)
-    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
-    const int lane = threadIdx.x & 63;
-    if (wave >= tiles_x * chunks_y * n_fields) return;
-    const int tx = wave % tiles_x;
-    const int ty = (wave / tiles_x) % chunks_y;
-    const int f = wave / (tiles_x * chunks_y);
-    if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;
-    const int c0 = out_lo + ty * rows_per_chunk;
-    const int c1 = min(c0 + rows_per_chunk, out_hi);
-    const int x0 = tx * W;
     WtLane L;
     L.ny = ny;
     L.cA = x0 - KH + 2 * lane;
@@ -293,16 +277,48 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
                                                           bot_reflect, coef, c4);
 }
 
+// FAST = tolerance mode (vk_set_stencil_mode(1)): FMA-contracted arithmetic and a
+// final pass without the base re-read; within ~1e-14 relative of the exact mode.
+template <int K, int PD, bool FINAL, bool FAST = false>
+__device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *dst,
+                                                const double *f0, int64_t field_stride, int ny,
+                                                int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
+                                                int bot_reflect, int rows_per_chunk, int tiles_x, int chunks_y,
+                                                int n_fields, double coef, const double *__restrict__ uniform,
+                                                const VkPsCouple &cp) {
+    constexpr int KH = K + (K & 1);
+    constexpr int W = WT_COLS - 2 * KH;
+    // (An XCD-contiguous tile order -- each XCD's L2 serving its tiles' shared
+    // halo columns -- measured 4 % slower on 4096^2: the halo re-reads already
+    // hit the die-level Infinity Cache, so plain round-robin order is kept.)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int lane = threadIdx.x & 63;
+    if (wave >= tiles_x * chunks_y * n_fields) return;
+    const int tx = wave % tiles_x;
+    const int ty = (wave / tiles_x) % chunks_y;
+    const int f = wave / (tiles_x * chunks_y);
+    const int c0 = out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    const int x0 = tx * W;
+    // agent coupling (vk_diffuse_coupled): the gather reads the plane before this pass
+    // changes anything; a uniform plane keeps its values and still takes the exchange
+    if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
+    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
+        diffuse_wl_tile_body<K, PD, FINAL, FAST>(src, dst, f0, field_stride, ny, in_lo, in_hi, top_reflect,
+                                                 bot_reflect, coef, f, x0, c0, c1, lane);
+    if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
+}
+
 // Aliasing: the FINAL pass writes the field it also reads as the base plane
 // (dst == f0, vk_diffuse), so only the source plane is __restrict__; each base
 // load feeds the store of the same cell, later in program order.
 #define VK_WL_PARAMS                                                                                           \
     const double *__restrict__ src, double *dst, const double *f0, int64_t field_stride, \
         int ny, int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect, int bot_reflect, int rows_per_chunk, \
-        int tiles_x, int chunks_y, int n_fields, double coef, const double *__restrict__ uniform
+        int tiles_x, int chunks_y, int n_fields, double coef, const double *__restrict__ uniform, const VkPsCouple cp
 #define VK_WL_ARGS                                                                                             \
     src, dst, f0, field_stride, ny, out_lo, out_hi, in_lo, in_hi, top_reflect, bot_reflect, rows_per_chunk,      \
-        tiles_x, chunks_y, n_fields, coef, uniform
+        tiles_x, chunks_y, n_fields, coef, uniform, cp
 
 #ifndef VK_WL_WAVES_ATTR
 #define VK_WL_WAVES_ATTR

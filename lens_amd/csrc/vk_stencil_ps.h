@@ -260,96 +260,6 @@ __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0
     ps_steady<K, PD, C, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);
 }
 
-// ---------------------------------------------------------------------------
-// Agent coupling inside a pass (vk_diffuse_coupled).  A wave owns the cells of
-// its output rows [c0, c1) x columns [x0, x0 + W); agents are stored in bin
-// order, so the agents of one such row segment are a contiguous run found from
-// the 16-column index cp.seg.  One lane per row; each lane takes its run in
-// batches of CB agents, issuing a batch's loads together (the run is ~7 agents
-// at C4), so a wave waits about two load latencies, not one per agent.
-// ---------------------------------------------------------------------------
-constexpr int CB = 16;
-
-// The first pass: gdst[grow[f] * gld + a] = the pre-step plane at bins[a]
-// (get_local_environments, diffusion_field.py:362-379), read before any pass
-// has written the plane -- the first pass reads `field` and writes a work buffer.
-template <int W>
-__device__ __forceinline__ void ps_couple_gather(const VkPsCouple &cp, const double *plane, int f, int ny, int x0,
-                                                 int c0, int c1, int lane) {
-    const int g = cp.grow[f];
-    if (g < 0) return;
-    double *dst = cp.gdst + (int64_t)g * cp.gld;
-    const int ce = min(x0 + W, ny);
-    for (int r = c0 + lane; r < c1; r += 64) {
-        const int bb = r * ny + x0, be = r * ny + ce;
-        int a = cp.seg[(int64_t)r * cp.nseg + (x0 >> 4)];
-        for (;;) {
-            int b[CB];
-#pragma unroll
-            for (int j = 0; j < CB; ++j) b[j] = a + j < cp.n ? cp.bins[a + j] : 0x7fffffff;
-            double v[CB];
-#pragma unroll
-            for (int j = 0; j < CB; ++j) v[j] = (b[j] >= bb && b[j] < be) ? plane[b[j]] : 0.0;
-#pragma unroll
-            for (int j = 0; j < CB; ++j)
-                if (b[j] >= bb && b[j] < be) dst[a + j] = v[j];
-            if (b[CB - 1] >= be) break;
-            a += CB;
-        }
-    }
-}
-
-// The final pass, after the wave's own stores: for each cell of the segment,
-// plane += counts[crow[f] * cld + a] / bva * 1000 for its agents in agent order
-// (update_field_with_exchange, registry.py:149-183, applied agent by agent as
-// k_exchange_sorted does -- the same bits).  The stores were made by other lanes
-// of this wave: a workgroup-scope fence orders them before the loads, which go
-// to L2 (agent-scope atomic loads skip the vector L1).
-template <int W>
-__device__ __forceinline__ void ps_couple_exchange(const VkPsCouple &cp, double *plane, int f, int ny, int x0,
-                                                   int c0, int c1, int lane) {
-    const int cr = cp.crow[f];
-    if (cr < 0) return;
-    const int64_t *cnt = cp.counts + (int64_t)cr * cp.cld;
-    const int ce = min(x0 + W, ny);
-    for (int r = c0 + lane; r < c1; r += 64) {
-        const int bb = r * ny + x0, be = r * ny + ce;
-        int a = cp.seg[(int64_t)r * cp.nseg + (x0 >> 4)];
-        int cur = -1;            // the cell being accumulated (its run may cross batches)
-        double acc = 0.0;
-        for (;;) {
-            int b[CB];
-            int64_t c[CB];
-#pragma unroll
-            for (int j = 0; j < CB; ++j) {
-                const bool in = a + j < cp.n;
-                b[j] = in ? cp.bins[a + j] : 0x7fffffff;
-                c[j] = in ? cnt[a + j] : 0;
-            }
-            double v[CB];        // the plane at each agent's cell (used by the first agent of a run)
-#pragma unroll
-            for (int j = 0; j < CB; ++j)
-                v[j] = (b[j] >= bb && b[j] < be && b[j] != (j ? b[j - 1] : cur))
-                           ? __hip_atomic_load(plane + b[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                           : 0.0;
-#pragma unroll
-            for (int j = 0; j < CB; ++j) {
-                if (b[j] >= bb && b[j] < be) {
-                    if (b[j] != cur) {
-                        if (cur >= 0) plane[cur] = acc;
-                        cur = b[j];
-                        acc = v[j];
-                    }
-                    acc = acc + ((double)c[j] / cp.bva) * 1000.0;
-                }
-            }
-            if (b[CB - 1] >= be) break;
-            a += CB;
-        }
-        if (cur >= 0) plane[cur] = acc;
-    }
-}
-
 // The stencil work of one wave: its tile of plane f, output rows [c0, c1)
 template <int K, int PD, int C, bool SC, int CP, int KH, int W>
 __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double *dst, int64_t field_stride, int ny,
@@ -418,15 +328,12 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     if (c0 >= c1) return;
     const int x0 = tx * W;
     // agent coupling: the gather reads the plane before this pass changes anything
-    if (cp.mode & 1) ps_couple_gather<W>(cp, src + (int64_t)f * field_stride, f, ny, x0, c0, c1, lane);
+    if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     // a uniform plane keeps its values (zero delta); the exchange still applies
     if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
         ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
                                           c4, cK, f, x0, c0, c1, lane);
-    if (cp.mode & 2) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        ps_couple_exchange<W>(cp, dst + (int64_t)f * field_stride, f, ny, x0, c0, c1, lane);
-    }
+    if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 
 template <int K, int PD, int C, int CP = 0>

@@ -2,7 +2,7 @@
 #include "vk_stencil_ps.h"
 
 // variant 20: 2 columns per lane, 4 rows prefetched
-void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS, const VkPsCouple *cp) {
+void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS) {
     (void)f0;   // the tolerance mode's final pass writes the new field as is
 #define VK_PS(KC) case KC: vk_ps::launch<KC, 4, 2>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp); break
     switch (k) {

@@ -6,7 +6,7 @@
 // plane a pass writes -- 134 MB at C4 -- can stay in the 256-MB MALL for the next pass).
 #include "vk_stencil_ps.h"
 
-void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS, const VkPsCouple *cp) {
+void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS) {
     (void)f0;
 #define VK_PSA(KC, PDC, CPC) \
     vk_ps::launch<KC, PDC, 2, CPC>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp)

@@ -14,11 +14,11 @@
 
 void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS) {
     if (k == 7)
-        vk_nt::launch<7, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
+        vk_nt::launch<7, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
     else if (k == 9)
-        vk_nt::launch<9, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
+        vk_nt::launch<9, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
     else if (k == 11)
-        vk_nt::launch<11, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
+        vk_nt::launch<11, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
     else if (k == 10)   // tolerance mode only; 3 rows prefetched keep it at 154 VGPRs (3 waves per SIMD)
-        vk_nt::launch_fast<10, 3>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm);
+        vk_nt::launch_fast<10, 3>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
 }

@@ -210,19 +210,17 @@ class Lattice:
 
     def coupled_plan_ok(self, timestep: float) -> bool:
         """Whether :meth:`diffuse_coupled` can run this step: a whole plane (no
-        row band) planned as two or more pair-sum passes -- the tolerance mode
-        with kernel variants 20-25 and pass depths 3..11 (vk_diffuse's planner,
-        restated; vk_diffuse_coupled makes the same decision and launches
-        nothing otherwise)."""
+        row band, at most 8 planes) planned as two or more fused passes and no
+        single-substep pass -- vk_diffuse's planner, restated (10-deep passes in
+        the tolerance mode's depth-10 setting, else odd depths); the library makes
+        the same decision and launches nothing otherwise."""
         if self.pad_top or self.pad_bot or not (self.edge_top and self.edge_bot) or len(self.molecules) > 8:
-            return False
-        if native._lib.vk_set_stencil_mode(-1) != 1 or native._lib.vk_set_stencil_kernel(-1, -1) < 20:
             return False
         n_sub = n_substeps(timestep, self.diffusion_dt)
         depth = native._lib.vk_set_stencil_depth(0)
-        if depth == 10 and n_sub % 10 == 0 and n_sub >= 20:
+        if depth == 10 and native._lib.vk_set_stencil_mode(-1) == 1 and n_sub % 10 == 0 and n_sub >= 20:
             return True
-        depth = 9 if depth == 10 else depth | 1
+        depth = min(9 if depth == 10 else depth | 1, 15)
         passes = (n_sub + depth - 1) // depth
         if (passes & 1) != (n_sub & 1):
             passes += 1
@@ -237,7 +235,7 @@ class Lattice:
             ks.append(k)
             j += k
             left -= 1
-        return len(ks) >= 2 and all(3 <= k <= 11 for k in ks)
+        return len(ks) >= 2 and min(ks) >= 2
 
     def diffuse_coupled(self, timestep: float, bin_lin, n_agents: int, seg, gather_rows, conc, count_rows,
                         counts, allreduce: Optional[Callable] = None, events=None):

@@ -6,7 +6,8 @@ bit for bit, step after step.  Covered: 10-deep and odd-depth plans, the
 stagger / cached-store variants, ragged planes (width not a multiple of 16 or
 of a tile), a plane narrower than one tile, several chunks per tile column,
 bins crowded past one load batch, uniform planes (the acetate plane starts at
-zero), graph replay, and the fallbacks (exact mode, agents out of bin order).
+zero), both arithmetic modes (pair-sum and variant-6 / plain-store wave tiles),
+graph replay, and the fallbacks (single-substep passes, agents out of bin order).
 """
 
 import os
@@ -98,6 +99,9 @@ CASES = {
     'd10_crowded': (33, 260, 2500, 90, 'fma', 10, 20, 12),
     'd10_narrow': (30, 50, 800, 40, 'fma', 10, 20, 0),
     'd7_tall_tiles': (70, 230, 4000, 0, 'fma', 7, 20, 64),
+    'exact_d9': (40, 300, 3000, 0, 'exact', 9, 6, 8),
+    'exact_d5_plain_stores': (33, 260, 2500, 90, 'exact', 5, 2, 12),
+    'exact_d10_setting': (40, 300, 3000, 0, 'exact', 10, 20, 0),
 }
 
 
@@ -129,17 +133,18 @@ def test_coupled_dopri5_graph_replay_equals_separate_launches(dev):
         _same(a, b, 'graph')
 
 
-def test_coupled_declined_exact_mode_and_unsorted(dev):
-    """The exact mode keeps the separate launches (vk_diffuse_coupled is planned
-    only over pair-sum passes); agents that moved out of bin order drop the index."""
-    with _stencil('exact', 9, 6, 8):
+def test_coupled_declined_single_substep_passes_and_unsorted(dev):
+    """One launch per substep (depth 1) keeps the separate launches (a
+    single-substep pass carries no coupling); agents that moved out of bin
+    order drop the index until they are sorted again."""
+    with _stencil('exact', 1, 6, 8):
         a, b = _pair(dev, 40, 300, 3000)
         assert not a[1].coupled_plan_ok(1.0)
         a[0].step(1.0)
         b[0].step(1.0)
         assert not a[0].last_step_coupled
         torch.cuda.synchronize()
-        _same(a, b, 'exact')
+        _same(a, b, 'depth 1')
     with _stencil('fma', 10, 20, 8):
         col, lat = a
         rng = np.random.default_rng(9)
