@@ -113,6 +113,9 @@ def parse(argv=None):
     p.add_argument('--graph', choices=['auto', 'on', 'off'], default='auto',
                    help='replay the timed steps from a captured HIP graph (auto: every single-GPU step that takes '
                         'no host decision, i.e. no division: C2, C3, C4)')
+    p.add_argument('--couple', action='store_true',
+                   help='carry the gather and the exchange in the first / final diffusion pass (vk_diffuse_coupled; '
+                        'same results; off by default: 1.533 vs 1.511 ms per C4 step, profiles/r04/r04h)')
     p.add_argument('--steps-per-launch', type=int, default=None,
                    help='held colonies (C2): timesteps per kernel launch (vk_step_dopri5_multi, each step bit for '
                         'bit the one-step kernel\'s); default = the steps per replayed graph')
@@ -437,6 +440,7 @@ def main():
     stencil_mode(args.stencil_mode)
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
+    col.fuse_coupling = bool(args.couple)
     halo_ex = allred = balancer = None
     if world > 1 and lat is not None:
         from lens_amd.distributed import make_halo_exchange, make_uniform_allreduce
@@ -522,11 +526,12 @@ def main():
                               'block replayed, halo exchange and uniform all-reduce eager',
                       'graphs_per_step': 1 + len(banded_step.graphs[1])}
     elif use_graph:
-        per_graph = next(g for g in (10, 5, 2, 1) if args.steps % g == 0)
-        # a held colony's agents do not couple between steps: a graph of 10 steps is
-        # one launch of 10 steps (vk_step_dopri5_multi) instead of 10 launches
+        # a held colony's agents do not couple between steps: a graph of up to 100 steps
+        # is one launch of that many steps (vk_step_dopri5_multi) instead of one per step
         multi_ok = (lat is None and col.cells is None and col.integrator == 'dopri5' and
                     col.engine.default_variant() == 2)
+        per_graph = next(g for g in ((100, 50, 20, 10, 5, 2, 1) if multi_ok else (10, 5, 2, 1))
+                         if args.steps % g == 0)
         spl = args.steps_per_launch if args.steps_per_launch is not None else (per_graph if multi_ok else 1)
         if spl > 1 and (not multi_ok or per_graph % spl):
             raise SystemExit('--steps-per-launch: a held DP45 colony, dividing the %d steps per graph' % per_graph)
@@ -757,6 +762,7 @@ def main():
                        'integrator': args.integrator, 'rtol': col.rtol, 'atol': col.atol,
                        'exchange': args.exchange, 'parallelism': 'row-bands x%d' % world,
                        'agents_in_bin_order': bool(nx and args.sort_agents),
+                       'coupled_passes': bool(args.couple and getattr(col, '_couple', None) is not None),
                        'stencil_mode': args.stencil_mode if nx else None,
                        'halo': (col.lattice.halo if col.lattice is not None else 0) if world > 1 else 0},
             'roofline': roofline,

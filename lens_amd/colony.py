@@ -69,9 +69,11 @@ class Colony:
         # banded lattices: the first halo exchange of a step runs on a comm stream
         # beside the kinetics and the gather (it writes only halo rows)
         self.overlap_halo = True
-        # lattice colonies stored in bin order: the gather and the exchange ride on
-        # the first and final diffusion passes (vk_diffuse_coupled; same results)
-        self.fuse_coupling = True
+        # lattice colonies stored in bin order: the gather and the exchange can ride on
+        # the first and final diffusion passes (vk_diffuse_coupled; same results).  Off
+        # by default: on one MI355X at C4 the coupled step ran 1.533 ms against 1.511
+        # with the separate launches (profiles/r04/r04h/couple_ab.log)
+        self.fuse_coupling = False
         self._couple = None
         self.last_step_coupled = False
         self._comm_stream = torch.cuda.Stream(self.device) if self.device.type == 'cuda' else None

@@ -92,7 +92,7 @@ int g_stencil_stagger = 0;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 27)) {
+    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 29)) {
         g_stencil_kernel = variant;
         g_stencil_stagger = variant == 23;
     }
@@ -264,7 +264,7 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         ok = ok && dsts[0] != S;
         if (ok) {
             // variants 26 / 27: one plane at a time, its passes back to back
-            const int nfl = g_stencil_kernel >= 26 ? 1 : n_fields;
+            const int nfl = (g_stencil_kernel == 26 || g_stencil_kernel == 27) ? 1 : n_fields;
             for (int f = 0; f < n_fields; f += nfl) {
                 const int64_t off = (int64_t)f * field_stride;
                 const double *cur = S + off;
@@ -383,7 +383,7 @@ extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, i
     hipStream_t s = (hipStream_t)stream;
     const int np = (int)ks.size();
     // variants 26 / 27: one plane at a time (vk_diffuse)
-    const int nfl = g_stencil_mode == 1 && g_stencil_kernel >= 26 ? 1 : n_fields;
+    const int nfl = g_stencil_mode == 1 && (g_stencil_kernel == 26 || g_stencil_kernel == 27) ? 1 : n_fields;
     for (int f = 0; f < n_fields; f += nfl) {
         const int64_t off = (int64_t)f * field_stride;
         double *pf = field + off, *w0 = work0 + off, *w1 = work1 + off;
@@ -399,10 +399,18 @@ extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, i
             if (last) dst = pf;
             else if (ten) dst = cur == w0 ? w1 : w0;
             else dst = (j + ks[p] - 1) & 1 ? w1 : w0;   // work[e & 1], e = this pass's last substep
-            c.mode = n_agents > 0 ? (p == 0 ? 1 : 0) | (last ? 2 : 0) : 0;
+            // variants 28 / 29 (A/B): the gather after the wave's stencil work instead of
+            // before it; 29 also stores the final pass through the caches (variant 24's
+            // stores), so the exchange's re-reads of the new plane can hit L2
+            const bool late = g_stencil_kernel == 28 || g_stencil_kernel == 29;
+            c.mode = n_agents > 0 ? (p == 0 ? (late ? 4 : 1) : 0) | (last ? 2 : 0) : 0;
             // the exact mode's final pass re-reads the step-start plane: vk_diffuse's f0
-            launch_pass(ks[p], s, cur, dst, last ? pf : nullptr, nfl, field_stride, ny, 0, rows, 0, rows, 0, rows - 1,
-                        coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
+            if (last && g_stencil_kernel == 29 && g_stencil_mode == 1 && ks[p] == 10)
+                vk_launch_ps_alt(24, 10, s, cur, dst, nullptr, nfl, field_stride, ny, 0, rows, 0, rows, 0, rows - 1,
+                                 coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
+            else
+                launch_pass(ks[p], s, cur, dst, last ? pf : nullptr, nfl, field_stride, ny, 0, rows, 0, rows, 0,
+                            rows - 1, coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
             const int rc = vk::launch_check("vk_diffuse_coupled kernel");
             if (rc) return rc;
             cur = dst;

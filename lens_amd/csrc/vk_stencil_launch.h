@@ -29,7 +29,8 @@ struct VkPsCouple {
     const int32_t *seg;
     int32_t nseg;
     int32_t n;                             // agents
-    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it
+    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it,
+                                           // bit 2: gather after the pass (its source plane is unchanged)
     double *gdst;                          // gather: gdst[grow[f] * gld + a] = plane f at bins[a] (pre-pass)
     int64_t gld;
     const int64_t *counts;                 // exchange: plane f += counts[crow[f] * cld + a] / bva * 1000

@@ -333,6 +333,7 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
         ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
                                           c4, cK, f, x0, c0, c1, lane);
+    if (cp.mode & 4) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 

@@ -99,6 +99,8 @@ CASES = {
     'd10_crowded': (33, 260, 2500, 90, 'fma', 10, 20, 12),
     'd10_narrow': (30, 50, 800, 40, 'fma', 10, 20, 0),
     'd7_tall_tiles': (70, 230, 4000, 0, 'fma', 7, 20, 64),
+    'd10_late_gather': (40, 300, 3000, 30, 'fma', 10, 28, 8),
+    'd10_late_gather_cached_final': (40, 300, 3000, 30, 'fma', 10, 29, 8),
     'exact_d9': (40, 300, 3000, 0, 'exact', 9, 6, 8),
     'exact_d5_plain_stores': (33, 260, 2500, 90, 'exact', 5, 2, 12),
     'exact_d10_setting': (40, 300, 3000, 0, 'exact', 10, 20, 0),
@@ -154,7 +156,7 @@ def test_coupled_declined_single_substep_passes_and_unsorted(dev):
         col.step(1.0)
         assert not col.last_step_coupled
         col.sort_by_bin()
-        assert col._couple is not None
+        assert col._couple is not None and col.fuse_coupling
         col.step(1.0)
         assert col.last_step_coupled
 
@@ -171,6 +173,7 @@ def test_c4_coupled_step_equals_separate_launches(dev):
     with _bench_stencil():
         a = bench.build_rank(args, 0, 1, dev)[:2]
         assert a[0]._couple is not None
+        a[0].fuse_coupling = True
         a[0].step(1.0)
         assert a[0].last_step_coupled
         torch.cuda.synchronize()
