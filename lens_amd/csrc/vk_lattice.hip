@@ -92,7 +92,7 @@ int g_stencil_stagger = 0;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 29)) {
+    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 32)) {
         g_stencil_kernel = variant;
         g_stencil_stagger = variant == 23;
     }
