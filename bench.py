@@ -65,13 +65,14 @@ SPLIT_STEPS = 6            # eager steps timed for the kinetics / diffusion spli
 def stencil_kernel_name(variant, depth, mode='exact'):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
     if mode == 'fma' and variant >= 20 and depth <= 11:
-        pd = {21: 2, 22: 6}.get(variant, 4) if depth in (9, 10) else 4
-        return 'vk_ps::k_diffuse_ps<%d, %d, 2, true>' % (depth, pd)
+        if variant == 30 and depth in (9, 10):
+            return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 4>' % depth
+        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true>' % depth
     if mode == 'fma' and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
     if mode == 'fma' and depth == 10:
         return 'vk_nt::k_diffuse_wl<10, 3, false, true>'
-    if variant in (6, 20, 21, 22) and depth in (7, 9, 11):
+    if variant in (6, 20, 30) and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false>' % depth
     return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 if variant == 2 else 6)
 

@@ -79,23 +79,19 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // Exact mode: 2 / 3 = wave tile lag-1 prefetching 3 / 6 rows, 6 = variant 3 with
 // streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
 // setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default),
-// 21 / 22 / 23 / 24 / 25 = its A/B alternates (2 / 6 rows prefetched; half-chunk stagger on odd tile
-// columns; cached stores; streaming loads), 26 / 27 = 24 / 20 one plane at a time (depth-10 plans),
+// 30 = its stage-0 ring held as 16-B vectors (a tie, kept as the no-drain alternate),
 // 6 = the variant-6 FMA form (4 FP64 ops per cell-substep instead of 3).
 // Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
 // 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
 // 7 (streaming loads), 8-11 (four columns per lane, compact boundary body, split
 // stages, LDS-crossbar neighbours), 12-16 (prefetch ring, buffer stores, zigzag
-// chunks, 6-row prefetch at depth 10) -- bit-exact, none faster.
+// chunks, 6-row prefetch at depth 10), 21-29 / 31 / 32 (pair-sum prefetch depths,
+// stagger, cache policies, one plane at a time, coupled-pass placements) -- none faster.
 static int g_stencil_kernel = 20;
-int g_stencil_stagger = 0;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || (variant >= 20 && variant <= 32)) {
-        g_stencil_kernel = variant;
-        g_stencil_stagger = variant == 23;
-    }
+    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 30) g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
 }
@@ -263,24 +259,16 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         }
         ok = ok && dsts[0] != S;
         if (ok) {
-            // variants 26 / 27: one plane at a time, its passes back to back
-            const int nfl = (g_stencil_kernel == 26 || g_stencil_kernel == 27) ? 1 : n_fields;
-            for (int f = 0; f < n_fields; f += nfl) {
-                const int64_t off = (int64_t)f * field_stride;
-                const double *cur = S + off;
-                for (int p = 0; p < P; ++p) {
-                    const int e = sub_begin + 10 * p + 9;
-                    const int grow = last_in_call - e;
-                    const int lo = max(lo_min, row_lo - grow);
-                    const int hi = min(hi_max, row_hi + grow);
-                    const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
-                    double *dst = dsts[p] + off;
-                    launch_pass(10, s, cur, dst, nullptr, nfl, field_stride, ny, lo, hi, in_lo, in_hi, top_reflect,
-                                bot_reflect, coeff_dt, uniform ? uniform + 2 * f : nullptr, nullptr);
-                    int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
-                    if (rc) return rc;
-                    cur = dst;
-                }
+            for (int p = 0; p < P; ++p) {
+                const int e = sub_begin + 10 * p + 9;
+                const int grow = last_in_call - e;
+                const int lo = max(lo_min, row_lo - grow);
+                const int hi = min(hi_max, row_hi + grow);
+                const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
+                launch_pass(10, s, p ? dsts[p - 1] : S, dsts[p], nullptr, n_fields, field_stride, ny, lo, hi, in_lo,
+                            in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr);
+                int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
+                if (rc) return rc;
             }
             return VK_OK;
         }
@@ -382,39 +370,21 @@ extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, i
     }
     hipStream_t s = (hipStream_t)stream;
     const int np = (int)ks.size();
-    // variants 26 / 27: one plane at a time (vk_diffuse)
-    const int nfl = g_stencil_mode == 1 && (g_stencil_kernel == 26 || g_stencil_kernel == 27) ? 1 : n_fields;
-    for (int f = 0; f < n_fields; f += nfl) {
-        const int64_t off = (int64_t)f * field_stride;
-        double *pf = field + off, *w0 = work0 + off, *w1 = work1 + off;
+    const double *cur = field;
+    for (int p = 0, j = 0; p < np; j += ks[p], ++p) {
+        const bool last = p == np - 1;
+        double *dst;
+        if (last) dst = field;
+        else if (ten) dst = cur == work0 ? work1 : work0;
+        else dst = (j + ks[p] - 1) & 1 ? work1 : work0;   // work[e & 1], e = this pass's last substep
         VkPsCouple c = cp;
-        for (int i = 0; i < nfl; ++i) {
-            c.grow[i] = cp.grow[f + i];
-            c.crow[i] = cp.crow[f + i];
-        }
-        const double *cur = pf;
-        for (int p = 0, j = 0; p < np; j += ks[p], ++p) {
-            const bool last = p == np - 1;
-            double *dst;
-            if (last) dst = pf;
-            else if (ten) dst = cur == w0 ? w1 : w0;
-            else dst = (j + ks[p] - 1) & 1 ? w1 : w0;   // work[e & 1], e = this pass's last substep
-            // variants 28 / 29 (A/B): the gather after the wave's stencil work instead of
-            // before it; 29 also stores the final pass through the caches (variant 24's
-            // stores), so the exchange's re-reads of the new plane can hit L2
-            const bool late = g_stencil_kernel == 28 || g_stencil_kernel == 29;
-            c.mode = n_agents > 0 ? (p == 0 ? (late ? 4 : 1) : 0) | (last ? 2 : 0) : 0;
-            // the exact mode's final pass re-reads the step-start plane: vk_diffuse's f0
-            if (last && g_stencil_kernel == 29 && g_stencil_mode == 1 && ks[p] == 10)
-                vk_launch_ps_alt(24, 10, s, cur, dst, nullptr, nfl, field_stride, ny, 0, rows, 0, rows, 0, rows - 1,
-                                 coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
-            else
-                launch_pass(ks[p], s, cur, dst, last ? pf : nullptr, nfl, field_stride, ny, 0, rows, 0, rows, 0,
-                            rows - 1, coeff_dt, uniform ? uniform + 2 * f : nullptr, &c);
-            const int rc = vk::launch_check("vk_diffuse_coupled kernel");
-            if (rc) return rc;
-            cur = dst;
-        }
+        c.mode = n_agents > 0 ? (p == 0 ? 1 : 0) | (last ? 2 : 0) : 0;
+        // the exact mode's final pass re-reads the step-start plane: vk_diffuse's f0
+        launch_pass(ks[p], s, cur, dst, last ? field : nullptr, n_fields, field_stride, ny, 0, rows, 0, rows, 0,
+                    rows - 1, coeff_dt, uniform, &c);
+        const int rc = vk::launch_check("vk_diffuse_coupled kernel");
+        if (rc) return rc;
+        cur = dst;
     }
     return VK_OK;
 }

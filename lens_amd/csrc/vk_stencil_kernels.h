@@ -306,7 +306,6 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
         diffuse_wl_tile_body<K, PD, FINAL, FAST>(src, dst, f0, field_stride, ny, in_lo, in_hi, top_reflect,
                                                  bot_reflect, coef, f, x0, c0, c1, lane);
-    if (cp.mode & 4) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 

@@ -13,7 +13,6 @@
 
 extern int g_stencil_rows;   // output rows per wave tile, 0 = auto (vk_lattice.hip, vk_set_stencil_kernel)
 extern int g_stencil_mode;   // 0 = bit-exact (default), 1 = tolerance / FMA (vk_set_stencil_mode)
-extern int g_stencil_stagger;  // pair-sum passes: odd tile columns' chunk grid shifted by half a chunk (variant 23)
 
 struct VkPsCouple;
 void vk_launch_wl3(VK_STENCIL_LAUNCH_ARGS);          // lag-1 wave tile, 3 rows prefetched
@@ -29,8 +28,7 @@ struct VkPsCouple {
     const int32_t *seg;
     int32_t nseg;
     int32_t n;                             // agents
-    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it,
-                                           // bit 2: gather after the pass (its source plane is unchanged)
+    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it
     double *gdst;                          // gather: gdst[grow[f] * gld + a] = plane f at bins[a] (pre-pass)
     int64_t gld;
     const int64_t *counts;                 // exchange: plane f += counts[crow[f] * cld + a] / bva * 1000
@@ -42,7 +40,7 @@ struct VkPsCouple {
 
 void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS);     // tolerance mode, pair-sum form (k = 3, 5, 7, 9, 11)
 void vk_launch_ps10(VK_STENCIL_LAUNCH_ARGS);   // the same, k = 10
-void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS);   // variant 20-27 dispatch (21-27: A/B alternates)
+void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS);   // variant 20 / 30 dispatch
 
 // ---------------------------------------------------------------------------
 // Agent coupling inside a pass (vk_diffuse_coupled), shared by both kernel

@@ -360,7 +360,6 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
-                                                    int stagger,
                                                     const double *__restrict__ uniform, const VkPsCouple cp) {
     constexpr int KH = (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
     constexpr int W = 64 * C - 2 * KH;           // columns written per tile
@@ -370,13 +369,8 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     const int tx = wave % tiles_x;
     const int ty = (wave / tiles_x) % chunks_y;
     const int f = wave / (tiles_x * chunks_y);
-    // stagger > 0: odd tile columns shift their chunk grid up by `stagger` rows
-    // (one chunk more, the first and last ones short), so the waves of a round
-    // do not run their fill phases in lockstep (chunks_y counts the extra one)
-    const int shift = (tx & 1) ? stagger : 0;
-    const int c0 = max(out_lo, out_lo + ty * rows_per_chunk - shift);
-    const int c1 = min(out_lo + (ty + 1) * rows_per_chunk - shift, out_hi);
-    if (c0 >= c1) return;
+    const int c0 = out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, out_hi);
     const int x0 = tx * W;
     // agent coupling: the gather reads the plane before this pass changes anything
     if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
@@ -384,7 +378,6 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
         ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
                                           c4, cK, f, x0, c0, c1, lane);
-    if (cp.mode & 4) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 
@@ -395,8 +388,7 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     constexpr int W = 64 * C - 2 * KH;
     const int tiles_x = (ny + W - 1) / W;
     const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
-    const int sh = g_stencil_stagger ? rch / 2 : 0;
-    const int chunks_y = (out_hi - out_lo + rch - 1) / rch + (sh ? 1 : 0);
+    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
     const double c4 = 1.0 - 4.0 * coef;
     VkPsCouple none = {};
@@ -407,10 +399,10 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, sh, mm, cpl);
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl);
     } else {
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, sh, mm, cpl);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl);
     }
 }
 

@@ -44,11 +44,12 @@ def stencil_depth(k: int = 0) -> int:
 
 
 def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
-    """Select the fused-pass kernel (0 = workgroup/LDS, 2/3/4 = wave/DPP lag-1 with 3/6/9
-    prefetched rows, 6 = 3 with streaming stores, the default; 12 = 6 with stage 0 on the
-    prefetch ring, 13 = 12 with branch-free buffer stores, 14 = 13 with 3 prefetched rows) and
-    output rows per tile
-    (0 = auto; -1 keeps).  Other numbers are ignored (retired variants)."""
+    """Select the fused-pass kernel and output rows per tile (0 = auto; -1 keeps);
+    returns the previous variant.  Exact mode: 2 / 3 = lag-1 wave tiles with 3 / 6
+    rows prefetched, 6 = 3 with streaming stores (the exact mode's default kernel).
+    Tolerance mode: 20 = pair-sum passes (the default), 30 = the same with the
+    stage-0 ring held as 16-B vectors, 6 = the 4-op FMA wave tiles.  Other numbers
+    are ignored (retired variants)."""
     native.load()
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
 

@@ -1,8 +1,8 @@
 """A/B of the coupled passes on the bench's C4 colony (bench.build_rank, bin order,
 DP45, the bench's stencil settings): graph-replayed steps with the gather and the
-exchange as separate launches, or carried by the first / final pass (variant 20),
-the gather after the wave's stencil work (28), and that plus a cached final pass
-(29).  Interleaved rounds in one process; prints ms per step.
+exchange as separate launches, or carried by the first / final pass (variant 20;
+round 4 also measured the gather after the wave's stencil work and a cached final
+pass, retired variants 28 / 29).  Interleaved rounds in one process; prints ms per step.
 
     python scripts/couple_ab.py [rounds]
 """
@@ -29,8 +29,7 @@ def main():
     build = types.SimpleNamespace(workload='c4', integrator='dopri5', halo=0, exchange='sorted',
                                   generic_kernel=False, agents=None, overlap_kinetics=False, sort_agents=True)
     col, lat, _ = bench.build_rank(build, 0, 1, dev)
-    configs = [('separate', 20, False), ('coupled', 20, True), ('coupled_late_gather', 28, True),
-               ('coupled_late_gather_cached_final', 29, True)]
+    configs = [('separate', 20, False), ('coupled', 20, True)]
     graphs = {}
     for name, variant, fused in configs:
         stencil_kernel(variant, rows)

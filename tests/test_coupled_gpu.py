@@ -3,7 +3,7 @@ riding on the first diffusion pass and the exchange on the final one must give
 exactly what the three separate launches give (vk_gather, the passes,
 vk_exchange_sorted) -- fields, external concentrations and every agent array
 bit for bit, step after step.  Covered: 10-deep and odd-depth plans, the
-stagger / cached-store variants, ragged planes (width not a multiple of 16 or
+vector-ring variant, ragged planes (width not a multiple of 16 or
 of a tile), a plane narrower than one tile, several chunks per tile column,
 bins crowded past one load batch, uniform planes (the acetate plane starts at
 zero), both arithmetic modes (pair-sum and variant-6 / plain-store wave tiles),
@@ -94,13 +94,10 @@ CASES = {
     # name: (nx, ny, agents, crowd, mode, depth, kernel, rows)
     'd10_ragged': (40, 300, 3000, 0, 'fma', 10, 20, 8),
     'd9_odd_plan': (40, 300, 3000, 0, 'fma', 9, 20, 8),
-    'd10_stagger': (40, 300, 3000, 0, 'fma', 10, 23, 8),
-    'd10_cached_stores': (40, 300, 3000, 0, 'fma', 10, 24, 8),
+    'd10_vector_ring': (40, 300, 3000, 0, 'fma', 10, 30, 8),
     'd10_crowded': (33, 260, 2500, 90, 'fma', 10, 20, 12),
     'd10_narrow': (30, 50, 800, 40, 'fma', 10, 20, 0),
     'd7_tall_tiles': (70, 230, 4000, 0, 'fma', 7, 20, 64),
-    'd10_late_gather': (40, 300, 3000, 30, 'fma', 10, 28, 8),
-    'd10_late_gather_cached_final': (40, 300, 3000, 30, 'fma', 10, 29, 8),
     'exact_d9': (40, 300, 3000, 0, 'exact', 9, 6, 8),
     'exact_d5_plain_stores': (33, 260, 2500, 90, 'exact', 5, 2, 12),
     'exact_d10_setting': (40, 300, 3000, 0, 'exact', 10, 20, 0),
