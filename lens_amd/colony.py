@@ -505,7 +505,57 @@ class Colony:
                 lat.exchange_atomic(self.bin_lin, self.n, self.counts, self.map_exch_count,
                                     self.map_exch_field)
 
-    def capture(self, dt: float = 1.0, steps: int = 1, stamps=None, steps_per_launch: int = 1):
+    def _overlap_ok(self):
+        """Whether :meth:`capture` can overlap a step's exchange with the next step's
+        kinetics (and the uniform probe with the gather)."""
+        lat = self.lattice
+        return (lat is not None and self.cells is None and not self.overlap_kinetics and not self.fuse_coupling
+                and self.device.type == 'cuda' and not (lat.pad_top or lat.pad_bot))
+
+    def _captured_steps_overlapped(self, dt, steps, stamps):
+        """The body of an overlapped capture (see :meth:`capture`).  Step k's exchange
+        scatter reads the counts buffer its own kinetics wrote, and runs on a side stream
+        while step k+1's kinetics writes the other buffer; the uniform probe runs on a
+        second side stream beside the gather.  Every read of the planes (probe, gather,
+        passes) waits for the previous exchange, so each step sees exactly the state a
+        sequential step would."""
+        lat = self.lattice
+        if getattr(self, '_x_stream', None) is None:
+            self._x_stream = torch.cuda.Stream(self.device)
+            self._p_stream = torch.cuda.Stream(self.device)
+        sx, sp = self._x_stream, self._p_stream
+        bufs = (self.counts, self._counts_alt)
+        pending = None
+        for k in range(steps):
+            stamp = None
+            if stamps is not None:
+                stamp = (lambda tag, k=k: native.check(native._lib.vk_timestamp(
+                    native.ptr(stamps), 3 * k + tag, native.stream_handle()), 'vk_timestamp'))
+                stamp(0)
+            self.counts = bufs[(steps - 1 - k) % 2]   # the last step writes the colony's own buffer
+            self.kinetics(dt)
+            if stamp is not None:
+                stamp(1)
+            main = torch.cuda.current_stream(self.device)
+            if pending is not None:
+                main.wait_event(pending)             # the previous step's exchange landed
+            sp.wait_stream(main)
+            with torch.cuda.stream(sp):
+                mm = lat.uniform_summary(None)       # the probe, beside the gather
+            self.gather_external()                   # pre-step field (one-step lag)
+            main.wait_stream(sp)
+            lat.diffuse(dt, summary=mm)
+            sx.wait_stream(main)
+            with torch.cuda.stream(sx):
+                self._step_exchange()                # this step's counts buffer
+                pending = torch.cuda.Event()
+                pending.record()
+            self._finish_step(dt)
+            if stamp is not None:
+                stamp(2)
+        torch.cuda.current_stream(self.device).wait_event(pending)
+
+    def capture(self, dt: float = 1.0, steps: int = 1, stamps=None, steps_per_launch: int = 1, overlap=False):
         """Capture ``steps`` timesteps into one HIP graph (torch.cuda.CUDAGraph)
         and return a function that replays them.
 
@@ -526,7 +576,14 @@ class Colony:
         :meth:`step_many` launches of that many steps instead.
         ``stamps`` (optional, a device int64 tensor of 3 * steps) records each
         replayed step's segment boundaries (:meth:`step`'s ``stamp``) at
-        [3k, 3k + 1, 3k + 2] -- vk_timestamp ticks, vk_wall_clock_khz per ms."""
+        [3k, 3k + 1, 3k + 2] -- vk_timestamp ticks, vk_wall_clock_khz per ms.
+        ``overlap`` (a single-GPU lattice colony without division): within the graph,
+        step k's exchange scatter runs on a side stream beside step k+1's kinetics (the
+        two alternate between two counts buffers), and the uniform probe beside the
+        gather.  The results are the sequential steps' bit for bit, and ``counts`` holds
+        the last replayed step's counts.  Off by default: at C4 the overlapped kernels
+        slow each other and each cross-stream dependency adds ~6 us, 1.518 against
+        1.515 ms per step (profiles/r04/r04k)."""
         lat = self.lattice
         if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
                 (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
@@ -540,19 +597,26 @@ class Colony:
             raise ValueError('Colony.capture: steps_per_launch must divide steps (and takes no stamps)')
         if spl > 1:
             self._step_buffers(spl)                 # allocated before the capture (graphs hold the pointers)
+        overlap = bool(overlap) and self._overlap_ok() and spl == 1
+        if overlap and (getattr(self, '_counts_alt', None) is None or self._counts_alt.shape != self.counts.shape):
+            self._counts_alt = torch.zeros_like(self.counts)
+        counts0 = self.counts
         graph = torch.cuda.CUDAGraph()
         t0, s0 = self.time, self.step_index
         layout, n = self._layout, self.n
         with torch.cuda.graph(graph):
             for k in range(steps // spl if spl > 1 else 0):
                 self.step_many(dt, spl)
-            for k in range(steps if spl == 1 else 0):
+            if overlap:
+                self._captured_steps_overlapped(dt, steps, stamps)
+            for k in range(steps if spl == 1 and not overlap else 0):
                 stamp = None
                 if stamps is not None:
                     stamp = (lambda tag, k=k: native.check(native._lib.vk_timestamp(
                         native.ptr(stamps), 3 * k + tag, native.stream_handle()), 'vk_timestamp'))
                 self.step(dt, stamp=stamp)
         self.time, self.step_index = t0, s0      # capture ran nothing
+        self.counts = counts0
 
         def replay():
             # the graph holds raw device pointers and the agent count of capture time

@@ -162,8 +162,11 @@ class Lattice:
 
     def diffuse(self, timestep: float, halo_exchange: Optional[Callable] = None,
                 allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None,
-                before_final: Optional[Callable] = None, halo_ready: bool = False):
+                before_final: Optional[Callable] = None, halo_ready: bool = False, summary=None):
         """Advance every plane by ``timestep`` (diffusion_field.py:385-407).
+
+        ``summary`` (optional): the vk_field_uniform summary of the step-start planes,
+        taken by the caller (the probe is then not run again).
 
         ``halo_ready``: the caller already ran the first block's halo exchange
         (see :meth:`exchange_first_halo`; the launch stream waits for it).
@@ -176,7 +179,9 @@ class Lattice:
         it reads ``fields`` and writes only the work planes."""
         n_sub = n_substeps(timestep, self.diffusion_dt)
         coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
-        mm = self.uniform_summary(allreduce) if skip_uniform else None
+        # ``summary``: a uniform summary the caller already took of the step-start planes
+        # (Colony's overlapped capture runs the probe beside the gather)
+        mm = summary if summary is not None else (self.uniform_summary(allreduce) if skip_uniform else None)
         if events is not None:
             events[0].record()
         banded = bool(self.pad_top or self.pad_bot)

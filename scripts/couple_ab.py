@@ -1,8 +1,9 @@
-"""A/B of the coupled passes on the bench's C4 colony (bench.build_rank, bin order,
-DP45, the bench's stencil settings): graph-replayed steps with the gather and the
-exchange as separate launches, or carried by the first / final pass (variant 20;
-round 4 also measured the gather after the wave's stencil work and a cached final
-pass, retired variants 28 / 29).  Interleaved rounds in one process; prints ms per step.
+"""A/B of how a graph-replayed C4 step is laid out on the bench's colony
+(bench.build_rank, bin order, DP45, the bench's stencil settings): sequential
+launches, the overlapped capture (step k's exchange beside step k+1's kinetics,
+the uniform probe beside the gather; Colony.capture(overlap=True)), and the coupled
+passes (gather / exchange inside the first / final pass).  Interleaved rounds in
+one process; prints ms per step.
 
     python scripts/couple_ab.py [rounds]
 """
@@ -29,12 +30,12 @@ def main():
     build = types.SimpleNamespace(workload='c4', integrator='dopri5', halo=0, exchange='sorted',
                                   generic_kernel=False, agents=None, overlap_kinetics=False, sort_agents=True)
     col, lat, _ = bench.build_rank(build, 0, 1, dev)
-    configs = [('separate', 20, False), ('coupled', 20, True)]
+    configs = [('sequential', False, False), ('overlapped', False, True), ('coupled', True, False)]
+    stencil_kernel(kernel, rows)
     graphs = {}
-    for name, variant, fused in configs:
-        stencil_kernel(variant, rows)
+    for name, fused, overlap in configs:
         col.fuse_coupling = fused
-        graphs[name] = col.capture(1.0, 10)
+        graphs[name] = col.capture(1.0, 10, overlap=overlap)
         graphs[name]()                     # upload + warm
     torch.cuda.synchronize()
     res = {name: [] for name, _, _ in configs}
