@@ -477,12 +477,69 @@ class Experiment:
         if bump:
             self._version += 1
 
+    def _apply_leaves(self, proc_path, up):
+        """Apply a :class:`lens_amd.process.AgentLeafUpdate` exactly as
+        :meth:`apply_update` applies ``up.as_dict()`` -- the other ports, then for each
+        agent the leaves under ``up.path`` with their schema updaters (a missing
+        agent, branch or leaf is skipped) -- without building the per-agent dicts.
+        An agent whose branch is not plain dicts goes through :meth:`_apply`."""
+        if up.rest:
+            self.apply_update(up.rest, proc_path)
+        if not up.ids:
+            return
+        _, parent, ppath, key = self._port_node(proc_path, 'agents')
+        agents = parent.get(key, _MISSING)
+        if not isinstance(agents, dict):
+            self.apply_update(up.as_dict(), proc_path)
+            return
+        apath = ppath + (key,)
+        updaters, keys, path = self.updaters, up.keys, up.path
+        leaf_updaters = self._leaf_updaters
+        for aid, row in zip(up.ids, up.rows):
+            node = agents.get(aid, _MISSING)
+            if node is _MISSING:
+                continue
+            for k in path:
+                if not isinstance(node, dict):
+                    break
+                node = node.get(k, _MISSING)
+                if node is _MISSING:
+                    break
+            if node is _MISSING:
+                continue
+            if not isinstance(node, dict):
+                one = dict(zip(keys, row))
+                for k in reversed(path):
+                    one = {k: one}
+                self._apply(agents, apath, aid, one, proc_path)
+                continue
+            cpath = apath + (aid,) + path
+            names = leaf_updaters.get(cpath)
+            if names is None:
+                names = leaf_updaters[cpath] = {}
+            for k, value in zip(keys, row):
+                cur = node.get(k, _MISSING)
+                if cur is _MISSING:
+                    continue
+                if isinstance(cur, dict):
+                    self._apply(node, cpath, k, value, proc_path)
+                    continue
+                name = names.get(k)
+                if name is None:
+                    name = names[k] = self._updater_at(cpath + (k,))
+                new = node[k] = updaters[name](cur, value, None)
+                if type(new) is dict:
+                    self._version += 1
+
     def send_updates(self, updates, derivers=None):
         self._deleted = {}
         for update, path in updates:
             raw = getattr(update, 'raw', None)
+            leaves = getattr(update, 'leaf_raw', None)
             if raw is not None:
                 self._apply_kinetics(path, *raw())       # BatchedInvoke: no update dict
+            elif leaves is not None:
+                self._apply_leaves(path, leaves())       # BatchedDiffusionField: columns
             else:
                 self.apply_update(update.get(), path)
         if derivers is None:

@@ -124,6 +124,20 @@ class _Immediate:
         return self.update
 
 
+class _ImmediateLeaves:
+    """A process's :class:`lens_amd.process.AgentLeafUpdate`: ``get()`` is the
+    reference's update dict, ``leaf_raw()`` the columns (lens_amd.engine.Experiment)."""
+
+    def __init__(self, raw):
+        self.raw_update = raw
+
+    def get(self, timeout=0):
+        return self.raw_update.as_dict()
+
+    def leaf_raw(self):
+        return self.raw_update
+
+
 class BatchedInvoke:
     """Drop-in value for ``Experiment(config['invoke'])``."""
 
@@ -135,6 +149,9 @@ class BatchedInvoke:
 
     def __call__(self, process, interval, states):
         if not isinstance(process, BatchedConvenienceKinetics):
+            raw = getattr(process, 'next_update_raw', None)
+            if raw is not None:
+                return _ImmediateLeaves(raw(interval, states))
             return _Immediate(process.next_update(interval, states))
         slot = self._next
         self._next += 1

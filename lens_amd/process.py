@@ -231,6 +231,30 @@ def _bin_sites(locations, n_bins, bounds):
     return i * n_bins[1] + j
 
 
+class AgentLeafUpdate:
+    """An update that sets the same leaves under every agent -- ``rest`` (the
+    update's other ports) plus, per agent id, ``agents[id][path...][key] = row[i]``
+    -- kept as columns.  ``as_dict()`` spells it out as the reference's nested
+    update dict; lens_amd.engine.Experiment applies it directly."""
+
+    __slots__ = ('rest', 'ids', 'path', 'keys', 'rows')
+
+    def __init__(self, rest, ids, path, keys, rows):
+        self.rest, self.ids, self.path, self.keys, self.rows = rest, ids, tuple(path), keys, rows
+
+    def as_dict(self):
+        update = dict(self.rest)
+        if self.ids:
+            agents = {}
+            for a, row in zip(self.ids, self.rows):
+                leaf = dict(zip(self.keys, row))
+                for k in reversed(self.path):
+                    leaf = {k: leaf}
+                agents[a] = leaf
+            update['agents'] = agents
+        return update
+
+
 class BatchedDiffusionField(ProcessBase):
     """GPU drop-in for ``DiffusionField`` (vivarium/processes/diffusion_field.py:209-407).
 
@@ -301,7 +325,10 @@ class BatchedDiffusionField(ProcessBase):
             k: {'_value': self.parameters[k], '_updater': 'set', '_emit': True} for k in ('bounds', 'n_bins', 'depth')}
         return schema
 
-    def next_update(self, timestep, states):
+    def next_update_raw(self, timestep, states):
+        """:meth:`next_update`'s update before it is spelled out per agent: an
+        :class:`AgentLeafUpdate` (lens_amd.engine.Experiment applies it without
+        building one dict per agent; ``as_dict()`` is the reference's update)."""
         from lens_amd import native
         torch = self._torch
         fields = states['fields']
@@ -325,9 +352,9 @@ class BatchedDiffusionField(ProcessBase):
                     'vk_gather')
             delta = lat.diffuse_delta(timestep)
             update['fields'] = {m: delta[f] for f, m in enumerate(self.molecule_ids)}
-            if agents:
-                cols = vals.cpu().numpy().T.tolist()
-                mols = self.molecule_ids
-                update['agents'] = {a: {'boundary': {'external': dict(zip(mols, col))}}
-                                    for a, col in zip(ids, cols)}
-        return update
+            raw = AgentLeafUpdate(update, ids if agents else [], ('boundary', 'external'), list(self.molecule_ids),
+                                  vals.cpu().numpy().T.tolist() if agents else [])
+        return raw
+
+    def next_update(self, timestep, states):
+        return self.next_update_raw(timestep, states).as_dict()

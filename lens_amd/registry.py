@@ -178,11 +178,34 @@ def make_update_field_with_exchange(avogadro: float = N_A_LEGACY):
     scipy.constants.N_A, lattice_utils.py:15: 6.022140857e23 under the scipy its
     fixtures were made with)."""
 
+    # every agent of a colony passes the same dimensions store values: their bin volume,
+    # bin counts and the field shape they imply are derived once per set of values
+    # (the entry holds the value objects, so identity stands for equality)
+    last = [None]
+
+    def derived(dims):
+        n_bins, bounds, depth = dims['n_bins'], dims['bounds'], dims['depth']
+        c = last[0]
+        if c is None or c[0] is not n_bins or c[1] is not bounds or c[2] is not depth:
+            nx, ny = int(n_bins[0]), int(n_bins[1])
+            c = last[0] = (n_bins, bounds, depth, _bin_volume(n_bins, bounds, depth) * avogadro, nx, ny, (nx, ny))
+        return c
+
     def update_field_with_exchange(current_value, new_value, states):
         location = states['global']['location']
-        n_bins = states['dimensions']['n_bins']
-        bounds = states['dimensions']['bounds']
-        depth = states['dimensions']['depth']
+        dims = states['dimensions']
+        if type(current_value) is DeviceField:
+            _, _, _, bva, nx, ny, shape = derived(dims)
+            # get_bin_site (lattice_utils.py:18-40), as _bin_site: floor(loc * n / bound) % n
+            i = int(math.floor(location[0] * nx / dims['bounds'][0])) % nx
+            j = int(math.floor(location[1] * ny / dims['bounds'][1])) % ny
+            if current_value._t.shape != shape:
+                raise ValueError('field shape %s does not match n_bins %s' % (current_value.shape, [nx, ny]))
+            current_value.queue_exchange(i * ny + j, int(new_value), bva)
+            return current_value
+        n_bins = dims['n_bins']
+        bounds = dims['bounds']
+        depth = dims['depth']
         i, j = _bin_site(location, n_bins, bounds)
         bva = _bin_volume(n_bins, bounds, depth) * avogadro
         if isinstance(current_value, DeviceField) or getattr(current_value, 'is_cuda', False):
