@@ -216,8 +216,8 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int
         raise ValueError('lds_ops=2 keeps species indices in 16 bits')
     ny = nd + nr
     lay = split_layout(t) if split_den else None
-    if split_den and (lay is None or lds_ops):
-        raise ValueError('split_den needs one round of <= 64 rate laws and lds_ops = 0')
+    if split_den and lay is None:
+        raise ValueError('split_den needs one round of <= 64 rate laws')
     SB = 0
     if lay is not None:
         lanes, dst, second, sets = lay

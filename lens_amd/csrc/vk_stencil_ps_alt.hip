@@ -4,7 +4,10 @@
 // Retired after their A/B (profiles/r04/r04a, r04f, r04i): 21 / 22
 // (2 / 6 rows prefetched), 23 (half-chunk stagger of odd tile columns), 24 / 25
 // (cached stores / streaming loads), 26 / 27 (one plane at a time), 28 / 29 (coupled
-// gather after the stencil, cached final pass), 31 / 32 (vector ring, 6 / 2 rows).
+// gather after the stencil, cached final pass), 31 / 32 (vector ring, 6 / 2 rows);
+// for row bands (profiles/r04/r04q-r04u): 34 (cached stores + vector ring), 37 (the
+// general body on every tile), 38 / 39 (8 / 12 rows prefetched) -- 33 (cached
+// stores) became the 10-deep pass's rule for MALL-sized passes (vk_stencil_ps10.hip).
 #include "vk_stencil_ps.h"
 
 void vk_launch_ps_alt(int variant, VK_STENCIL_LAUNCH_ARGS) {

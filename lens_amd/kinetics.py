@@ -53,7 +53,7 @@ class KineticsEngine:
             # instead, while its padded per-lane operands fit the register file
             if wave_registers(self.table) > self.WAVE_REGISTER_LIMIT:
                 return self
-            split = int(bool(self.WAVE_SPLIT_DEN) and not self.WAVE_LDS_OPS and split_layout(self.table) is not None)
+            split = int(bool(self.WAVE_SPLIT_DEN) and split_layout(self.table) is not None)
             # 3 waves per SIMD where the split layout's estimate leaves room (C5: 162 -> 167
             # VGPRs, 16 spilled, 0.63 VALU busy); larger networks keep 2
             wpe = self.WAVE_WAVES_PER_SIMD or (3 if split and wave_registers(self.table, True) <= 165 else 2)
@@ -70,7 +70,10 @@ class KineticsEngine:
     WAVE_PAD_WRITES = 1         # 1: branch-free LDS publishes (padding lanes write a scratch slot;
                                 # C5 113.5 -> 111.9 ms, profiles/r03/r03e_c5_probe.log)
     WAVE_LDS_OPS = 0            # 1: denominator 1/Km and stoichiometry read from LDS tables (fewer VGPRs);
-                                # 2: also the denominator member indices
+                                # 2: also the denominator member indices.  With split denominators
+                                # (bit-identical): C5 98.6 / 113.6 ms at 3 waves/SIMD, 175.7 / 123.7 at 4,
+                                # against 91.6 ms for 0 (profiles/r04/r04p_c5.log): occupancy is not what
+                                # bounds the kernel
     WAVE_SPLIT_DEN = 1          # 1: the heaviest denominators split over lanes l and l + 32 (codegen.split_layout),
                                 # summed in set order (bit-identical); C5 112.0 -> 87.3 ms at 3 waves/SIMD
                                 # (profiles/r03/r03i_c5_probe.log)

@@ -65,8 +65,21 @@ def band_ms(world, halo, rows, variant, depth):
             src[:, lat.row_hi:lat.row_hi + h].copy_(bufs[3])
 
     ms = time_steps(lambda: lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None))
+    # the same step with its launch sequence replayed from one HIP graph (the stand-in
+    # exchange included), as the bench replays a band's halo blocks: the GPU's time
+    # without the host's issue of ~20 launches per step
+    lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
+    torch.cuda.synchronize()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
+        lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    g.replay()
+    graph_ms = time_steps(g.replay)
     del lat
-    return band, ms
+    return band, ms, graph_ms
 
 
 def main():
@@ -76,12 +89,18 @@ def main():
         whole = whole_plane_ms()
         print(json.dumps({'world': world, 'whole_plane_ms': round(whole, 4), 'ideal_ms': round(whole / world, 4)}),
               flush=True)
+        for v in os.environ.get('WHOLE_VARIANTS', '').split(','):   # A/B of the whole plane's kernel: variant[:rows]
+            if v:
+                v, r = (int(x) for x in (v + ':34').split(':')[:2])
+                print(json.dumps({'world': 1, 'variant': v, 'rows': r, 'whole_plane_ms': round(whole_plane_ms(v, rows=r), 4)}),
+                      flush=True)
         for spec in sys.argv[3].split(','):
             halo, rows, variant, depth = (int(x) for x in spec.split(':'))
-            band, ms = band_ms(world, halo, rows, variant, depth)
+            band, ms, graph_ms = band_ms(world, halo, rows, variant, depth)
             print(json.dumps({'world': world, 'band': list(band), 'halo': halo, 'rows': rows, 'variant': variant,
                               'depth': depth, 'ms_per_step': round(ms, 4),
-                              'efficiency': round(whole / world / ms, 3)}), flush=True)
+                              'efficiency': round(whole / world / ms, 3), 'graph_ms_per_step': round(graph_ms, 4),
+                              'graph_efficiency': round(whole / world / graph_ms, 3)}), flush=True)
         return
     halo, rows = int(sys.argv[2]), int(sys.argv[3])
     variant = int(sys.argv[4]) if len(sys.argv) > 4 else 20
@@ -89,10 +108,11 @@ def main():
     mode = sys.argv[6] if len(sys.argv) > 6 else 'fma'
     stencil_mode(mode)
     whole = whole_plane_ms()
-    band, ms = band_ms(world, halo, rows, variant, depth)
-    print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step; whole plane %.3f ms (live), '
-          'ideal %.3f = 1/N of it, diffusion efficiency %.2f' % (world, band, halo, rows, variant, depth, mode, ms,
-                                                                 whole, whole / world, whole / world / ms))
+    band, ms, graph_ms = band_ms(world, halo, rows, variant, depth)
+    print('N=%d band=%s halo=%d rows=%d variant=%d depth=%d mode=%s: %.3f ms/step (graph %.3f); whole plane %.3f ms '
+          '(live), ideal %.3f = 1/N of it, diffusion efficiency %.2f (graph %.2f)'
+          % (world, band, halo, rows, variant, depth, mode, ms, graph_ms, whole, whole / world, whole / world / ms,
+             whole / world / graph_ms))
 
 
 if __name__ == '__main__':
