@@ -99,12 +99,15 @@ class Experiment:
         self._ports: Dict[int, Tuple] = {}          # id(process) -> (process, its port names)
         self._updater_cache: Dict[Tuple, str] = {}  # resolved schema updater per leaf path
         self._leaf_updaters: Dict[Tuple, Dict] = {}  # branch path -> {leaf key: updater name}
+        # (agents path, branch) -> {agent id: that agent's _leaf_updaters entry} (no per-agent path tuple)
+        self._agent_leaf_names: Dict[Tuple, Dict] = {}
         # (process path, port) -> (structure version, parent node, parent path, key): the
         # store node a port resolves to.  Value updates replace leaves only; the version
         # moves whenever a dict-valued node is replaced or the schema registers nodes, and
         # an entry from an older version is resolved again.
         self._port_nodes: Dict[Tuple, Tuple] = {}
         self._plans: Dict[Tuple, Tuple] = {}        # process path -> (version, process, kinetics plan)
+        self._state_nodes: Dict[Tuple, Tuple] = {}  # process path -> (version, process, [(port, parent, key)])
         self._version = 0
         self.dividers: Dict[Tuple, object] = {}   # store path (with '*' globs) -> schema _divider
         self._div_globs: List[Tuple] = []
@@ -152,8 +155,7 @@ class Experiment:
         if not isinstance(schema, dict):
             return
         self._version += 1
-        self._updater_cache.clear()
-        self._leaf_updaters.clear()
+        self._clear_leaf_caches()
         keys = [k for k in schema if not k.startswith('_')]
         if ('_default' in schema or '_value' in schema or '_updater' in schema or '_divider' in schema) and not keys:
             if '_updater' in schema:           # a schema without one keeps the store's updater
@@ -211,11 +213,22 @@ class Experiment:
         return ent
 
     def process_states(self, path, proc):
-        out = {}
-        for port in self._port_names(proc):
-            ent = self._port_node(path, port)
-            out[port] = ent[1][ent[3]]
-        return out
+        # (parent node, key) per port, resolved once per (process path, structure version)
+        # and kept on the process itself: one attribute read per call instead of a lookup
+        # in a colony-sized dict keyed by path tuples (their hashes are not cached)
+        pd = getattr(proc, '__dict__', None)
+        ent = pd.get('_engine_state_nodes') if pd is not None else self._state_nodes.get(path)
+        if ent is None or ent[0] is not self or ent[1] != path or ent[2] != self._version:
+            nodes = []
+            for port in self._port_names(proc):
+                e = self._port_node(path, port)
+                nodes.append((port, e[1], e[3]))
+            ent = (self, path, self._version, nodes)
+            if pd is not None:
+                pd['_engine_state_nodes'] = ent
+            else:
+                self._state_nodes[path] = ent
+        return {port: parent[key] for port, parent, key in ent[3]}
 
     def apply_update(self, update, proc_path):
         for port, value in update.items():
@@ -293,11 +306,17 @@ class Experiment:
             self._divide(cpath, update['_divide'])
         return {k: v for k, v in update.items() if k not in ('_delete', '_add', '_generate', '_divide')}
 
+    def _clear_leaf_caches(self):
+        self._updater_cache.clear()
+        self._leaf_updaters.clear()
+        for names in self._agent_leaf_names.values():   # emptied in place: a running
+            names.clear()                               # _apply_leaves holds them
+        self._agent_leaf_names.clear()
+
     def _structure_changed(self):
         self._version += 1
         self._structure += 1
-        self._updater_cache.clear()
-        self._leaf_updaters.clear()
+        self._clear_leaf_caches()
 
     def _establish(self, path):
         node = self.state
@@ -405,8 +424,9 @@ class Experiment:
         unpack_update would build (internal deltas, fluxes, then the fields'
         inline update_field_with_exchange).  None when a target is not a plain
         leaf (the generic path handles it)."""
-        ent = self._plans.get(proc_path)
-        if ent is not None and ent[0] == self._version and ent[1] is process:
+        pd = getattr(process, '__dict__', None)
+        ent = pd.get('_engine_kinetics_plan') if pd is not None else self._plans.get(proc_path)
+        if ent is not None and ent[0] == self._version and ent[1] is process and ent[3] is self and ent[4] == proc_path:
             return ent[2]
         t = process.table
         plan = None
@@ -427,7 +447,9 @@ class Experiment:
                     elif isinstance(cur, dict):
                         raise LookupError
                     else:
-                        out.append((node, k, self.updaters[self._updater_at(cpath + (k,))]))
+                        fn = self.updaters[self._updater_at(cpath + (k,))]
+                        # kind 0 / 1: the built-in accumulate / set, applied inline
+                        out.append((node, k, fn, 0 if fn is _accumulate else (1 if fn is _set else 2)))
                 return out
             dyn = [leaves(port, [name])[0] for port, name in t.species[:t.n_dyn]]
             flux = leaves('fluxes', t.reaction_ids)
@@ -440,16 +462,21 @@ class Experiment:
                 e = self._port_node(proc_path, pp)
                 states[up] = e[1][e[3]]
             exch = self.updaters['update_field_with_exchange']
+            site = getattr(exch, 'site', None)           # lens_amd.registry's updater: one bin per agent
             fields = []
             for mol in t.external_ids:
                 cur = fnode.get(mol, _MISSING)
                 if isinstance(cur, dict):
                     raise LookupError
                 fields.append(None if cur is _MISSING else (fnode, mol))
-            plan = (dyn, flux, fields, exch, states)
+            plan = (dyn, flux, fields, exch, states, site)
         except (LookupError, KeyError, TypeError):
             plan = None
-        self._plans[proc_path] = (self._version, process, plan)
+        ent = (self._version, process, plan, self, proc_path)
+        if pd is not None:
+            pd['_engine_kinetics_plan'] = ent
+        else:
+            self._plans[proc_path] = ent
         return plan
 
     def _apply_kinetics(self, proc_path, process, fluxes, deltas, counts):
@@ -457,22 +484,46 @@ class Experiment:
         if plan is None:
             self.apply_update(process.unpack_update(fluxes, deltas, counts), proc_path)
             return
-        dyn, flux, fields, exch, states = plan
+        dyn, flux, fields, exch, states, site = plan
         bump = False
+        # the updaters in apply_update's order; accumulate / set inline (a float or
+        # numpy scalar sum / value is never a dict, so the structure cannot move)
         for tgt, d in zip(dyn, deltas):
             if tgt is not None:
-                node, k, fn = tgt
-                new = node[k] = fn(node[k], d, None)
-                bump |= type(new) is dict
+                node, k, fn, kind = tgt
+                if kind == 0:
+                    node[k] = node[k] + d
+                elif kind == 1:
+                    node[k] = d
+                else:
+                    new = node[k] = fn(node[k], d, None)
+                    bump |= type(new) is dict
         for tgt, f in zip(flux, fluxes):
             if tgt is not None:
-                node, k, fn = tgt
-                new = node[k] = fn(node[k], np.float64(f), None)
-                bump |= type(new) is dict
+                node, k, fn, kind = tgt
+                if kind == 0:
+                    node[k] = node[k] + np.float64(f)
+                elif kind == 1:
+                    node[k] = np.float64(f)
+                else:
+                    new = node[k] = fn(node[k], np.float64(f), None)
+                    bump |= type(new) is dict
+        where = None
         for tgt, c in zip(fields, counts):
             if tgt is not None:
                 node, mol = tgt
-                new = node[mol] = exch(node[mol], c, states)
+                cur = node[mol]
+                if site is not None and type(cur) is DeviceField:
+                    # update_field_with_exchange on a device field, with the agent's
+                    # bin derived once for all its molecules
+                    if where is None:
+                        where = site(states)
+                    if cur._t.shape != where[2]:
+                        raise ValueError('field shape %s does not match n_bins %s'
+                                         % (cur.shape, list(where[2])))
+                    cur.queue_exchange(where[0], int(c), where[1])
+                    continue
+                new = node[mol] = exch(cur, c, states)
                 bump |= isinstance(new, dict)
         if bump:
             self._version += 1
@@ -495,6 +546,9 @@ class Experiment:
         apath = ppath + (key,)
         updaters, keys, path = self.updaters, up.keys, up.path
         leaf_updaters = self._leaf_updaters
+        by_agent = self._agent_leaf_names.get((apath, path))
+        if by_agent is None:
+            by_agent = self._agent_leaf_names[(apath, path)] = {}
         for aid, row in zip(up.ids, up.rows):
             node = agents.get(aid, _MISSING)
             if node is _MISSING:
@@ -513,10 +567,13 @@ class Experiment:
                     one = {k: one}
                 self._apply(agents, apath, aid, one, proc_path)
                 continue
-            cpath = apath + (aid,) + path
-            names = leaf_updaters.get(cpath)
+            names = by_agent.get(aid)
             if names is None:
-                names = leaf_updaters[cpath] = {}
+                cpath = apath + (aid,) + path
+                names = leaf_updaters.get(cpath)
+                if names is None:
+                    names = leaf_updaters[cpath] = {}
+                by_agent[aid] = names
             for k, value in zip(keys, row):
                 cur = node.get(k, _MISSING)
                 if cur is _MISSING:
@@ -527,7 +584,13 @@ class Experiment:
                 name = names.get(k)
                 if name is None:
                     name = names[k] = self._updater_at(cpath + (k,))
-                new = node[k] = updaters[name](cur, value, None)
+                fn = updaters[name]
+                if fn is _set:
+                    node[k] = value
+                    if type(value) is dict:
+                        self._version += 1
+                    continue
+                new = node[k] = cur + value if fn is _accumulate else fn(cur, value, None)
                 if type(new) is dict:
                     self._version += 1
 
@@ -582,18 +645,20 @@ class Experiment:
                 live = {p for p, _ in processes}
                 front = {p: f for p, f in front.items() if p in live}
             full_step = INFINITY
+            invoke, states_of = self.invoke, self.process_states
             for path, proc in processes:
-                if path not in front:
-                    front[path] = {'time': time, 'update': None}
-                process_time = front[path]['time']
+                adv = front.get(path)
+                if adv is None:
+                    adv = front[path] = {'time': time, 'update': None}
+                process_time = adv['time']
                 if process_time <= time:
                     future = min(process_time + proc.local_timestep(), interval)
                     timestep = future - process_time
-                    pending = self.invoke(proc, timestep, self.process_states(path, proc))
+                    pending = invoke(proc, timestep, states_of(path, proc))
                     if timestep < full_step:
                         full_step = timestep
-                    front[path]['time'] = future
-                    front[path]['update'] = (pending, path)
+                    adv['time'] = future
+                    adv['update'] = (pending, path)
             if full_step == INFINITY:
                 next_event = interval
                 for _ in front.keys():

@@ -219,7 +219,19 @@ def make_update_field_with_exchange(avogadro: float = N_A_LEGACY):
         delta[i, j] += new_value / bva * 1000.0
         return current_value + delta
 
+    def site(states):
+        """(linear bin, bin_volume * N_A, field shape) of the agent whose port
+        states are ``states`` -- what one call above derives for a DeviceField, for
+        a caller that queues several molecules of one agent at once."""
+        location = states['global']['location']
+        dims = states['dimensions']
+        _, _, _, bva, nx, ny, shape = derived(dims)
+        i = int(math.floor(location[0] * nx / dims['bounds'][0])) % nx
+        j = int(math.floor(location[1] * ny / dims['bounds'][1])) % ny
+        return i * ny + j, bva, shape
+
     update_field_with_exchange.avogadro = avogadro
+    update_field_with_exchange.site = site
     return update_field_with_exchange
 
 

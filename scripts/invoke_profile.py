@@ -20,6 +20,9 @@ import torch  # noqa: E402
 from invoke_throughput import build  # noqa: E402
 
 
+REPS = int(os.environ.get('INVOKE_REPS', '3'))
+
+
 def run(n, steps=3, gc_on=True, profile=False):
     from lens_amd.engine import Experiment
     from lens_amd.invoke import BatchedInvoke
@@ -32,7 +35,7 @@ def run(n, steps=3, gc_on=True, profile=False):
         gc.disable()
     prof = cProfile.Profile() if profile else None
     best = float('inf')
-    for _ in range(1 if prof else 3):       # min of 3 timed calls: the box's host timing is noisy
+    for _ in range(1 if prof else REPS):    # min of REPS timed calls: the box's host timing is noisy
         t0 = time.perf_counter()
         if prof:
             prof.enable()
@@ -43,7 +46,7 @@ def run(n, steps=3, gc_on=True, profile=False):
         best = min(best, time.perf_counter() - t0)
     gc.enable()
     print('agents %6d  gc %-3s  %.1f us per agent-step (min of %d calls of %d steps)'
-          % (n, 'on' if gc_on else 'off', best / (n * steps) * 1e6, 1 if prof else 3, steps), flush=True)
+          % (n, 'on' if gc_on else 'off', best / (n * steps) * 1e6, 1 if prof else REPS, steps), flush=True)
     if prof:
         s = io.StringIO()
         st = pstats.Stats(prof, stream=s)

@@ -195,7 +195,8 @@ def test_direct_kinetics_apply_equals_update_dict():
         del exp.state['agents']['a3']['fluxes'][sorted(exp.state['agents']['a3']['fluxes'])[0]]
         exp.update(3.0)
         if with_raw:
-            assert len(exp._plans) == 6 and all(e[2] is not None for e in exp._plans.values())
+            plans = [p['kinetics'].__dict__.get('_engine_kinetics_plan') for p in exp.processes['agents'].values()]
+            assert len(plans) == 6 and all(e is not None and e[2] is not None for e in plans)
         states.append(exp.state)
 
     def same(x, y):
