@@ -99,7 +99,8 @@ class Experiment:
         self._ports: Dict[int, Tuple] = {}          # id(process) -> (process, its port names)
         self._updater_cache: Dict[Tuple, str] = {}  # resolved schema updater per leaf path
         self._leaf_updaters: Dict[Tuple, Dict] = {}  # branch path -> {leaf key: updater name}
-        # (agents path, branch) -> {agent id: that agent's _leaf_updaters entry} (no per-agent path tuple)
+        # (agents path, branch) -> {agent id: (version, its leaf branch node, its _leaf_updaters
+        # entry, its branch path)}: no per-agent path tuple or walk while the structure stands
         self._agent_leaf_names: Dict[Tuple, Dict] = {}
         # (process path, port) -> (structure version, parent node, parent path, key): the
         # store node a port resolves to.  Value updates replace leaves only; the version
@@ -309,8 +310,8 @@ class Experiment:
     def _clear_leaf_caches(self):
         self._updater_cache.clear()
         self._leaf_updaters.clear()
-        for names in self._agent_leaf_names.values():   # emptied in place: a running
-            names.clear()                               # _apply_leaves holds them
+        for per_agent in self._agent_leaf_names.values():   # emptied in place: a running
+            per_agent.clear()                               # _apply_leaves holds them
         self._agent_leaf_names.clear()
 
     def _structure_changed(self):
@@ -550,30 +551,34 @@ class Experiment:
         if by_agent is None:
             by_agent = self._agent_leaf_names[(apath, path)] = {}
         for aid, row in zip(up.ids, up.rows):
-            node = agents.get(aid, _MISSING)
-            if node is _MISSING:
-                continue
-            for k in path:
-                if not isinstance(node, dict):
-                    break
-                node = node.get(k, _MISSING)
+            # the agent's leaf branch, its path and its leaf updater names, kept per
+            # agent until the store's structure moves (the port-node rule)
+            ent = by_agent.get(aid)
+            if ent is not None and ent[0] == self._version:
+                node, names, cpath = ent[1], ent[2], ent[3]
+            else:
+                node = agents.get(aid, _MISSING)
                 if node is _MISSING:
-                    break
-            if node is _MISSING:
-                continue
-            if not isinstance(node, dict):
-                one = dict(zip(keys, row))
-                for k in reversed(path):
-                    one = {k: one}
-                self._apply(agents, apath, aid, one, proc_path)
-                continue
-            names = by_agent.get(aid)
-            if names is None:
+                    continue
+                for k in path:
+                    if not isinstance(node, dict):
+                        break
+                    node = node.get(k, _MISSING)
+                    if node is _MISSING:
+                        break
+                if node is _MISSING:
+                    continue
+                if not isinstance(node, dict):
+                    one = dict(zip(keys, row))
+                    for k in reversed(path):
+                        one = {k: one}
+                    self._apply(agents, apath, aid, one, proc_path)
+                    continue
                 cpath = apath + (aid,) + path
                 names = leaf_updaters.get(cpath)
                 if names is None:
                     names = leaf_updaters[cpath] = {}
-                by_agent[aid] = names
+                by_agent[aid] = (self._version, node, names, cpath)
             for k, value in zip(keys, row):
                 cur = node.get(k, _MISSING)
                 if cur is _MISSING:

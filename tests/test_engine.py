@@ -208,3 +208,61 @@ def test_direct_kinetics_apply_equals_update_dict():
 
     assert same(states[0], states[1])
     assert not np.array_equal(states[0]['fields']['glc__D_e'], np.ones((8, 4)))     # the exchange landed
+
+
+class _LeafWriter(Process):
+    """Writes every listed agent's boundary.external leaves each step: rows of
+    seeded values over a key list that grows after the first step (a key no
+    agent had resolved yet), as an AgentLeafUpdate (``leaf_raw``) or as the
+    reference's update dict only."""
+    name = 'leaf_writer'
+
+    def __init__(self, ids, with_raw):
+        super().__init__({'time_step': 1.0})
+        self.ids, self.with_raw, self.calls = ids, with_raw, 0
+        self.rng = np.random.default_rng(11)
+
+    def ports_schema(self):
+        return {'agents': {'*': {'boundary': {'external': {
+            'glc': {'_default': 0.0, '_updater': 'set'},
+            'ac': {'_default': 0.0},                                   # accumulate
+            'lac': {'_default': 1.0, '_updater': 'halve_then_add'}}}}}}
+
+    def next_update_raw(self, timestep, states):
+        from lens_amd.process import AgentLeafUpdate
+        self.calls += 1
+        keys = ['glc', 'ac'] if self.calls == 1 else ['glc', 'ac', 'lac', 'absent']
+        rows = self.rng.normal(size=(len(self.ids), len(keys))).tolist()
+        return AgentLeafUpdate({}, list(self.ids), ('boundary', 'external'), keys, rows)
+
+
+class _LeafInvoke:
+    def __init__(self, with_raw):
+        self.with_raw = with_raw
+
+    def __call__(self, process, interval, states):
+        up = process.next_update_raw(interval, states)
+        if self.with_raw:
+            return type('L', (), {'get': lambda s, timeout=0: up.as_dict(), 'leaf_raw': lambda s: up})()
+        return type('D', (), {'get': lambda s, timeout=0: up.as_dict()})()
+
+
+def test_leaf_columns_apply_equals_update_dict():
+    """Experiment._apply_leaves (an AgentLeafUpdate applied as columns, with its
+    per-agent branch cache) against apply_update of the same update's dict: set,
+    accumulate and a custom updater; a key list that grows on the second step;
+    an agent id with no store, an agent without the branch and a leaf the store
+    lacks -- identical stores after 3 steps."""
+    states = []
+    for with_raw in (True, False):
+        agents = {'a%d' % i: {'boundary': {'external': {'glc': 1.0 * i, 'ac': 0.5, 'lac': 2.0}}} for i in range(5)}
+        agents['a3'] = {'other': {}}                       # no boundary branch
+        del agents['a2']['boundary']['external']['ac']     # a missing leaf
+        ids = ['a0', 'a1', 'a2', 'a3', 'a4', 'ghost']
+        exp = Experiment({'processes': {'w': _LeafWriter(ids, with_raw)}, 'topology': {'w': {'agents': ('agents',)}},
+                          'initial_state': {'agents': agents}, 'invoke': _LeafInvoke(with_raw)})
+        exp.updaters['halve_then_add'] = lambda cur, new, st: cur * 0.5 + new
+        exp.update(3.0)
+        states.append(exp.state)
+    assert states[0] == states[1]
+    assert 'absent' not in states[0]['agents']['a0']['boundary']['external']
