@@ -62,11 +62,15 @@ KREMLING_NY = 15
 SPLIT_STEPS = 6            # eager steps timed for the kinetics / diffusion split (the first is dropped)
 
 
-def stencil_kernel_name(variant, depth, mode='exact'):
-    """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse)."""
+def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
+    """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse).
+    ``pass_bytes`` (source + destination rows of one pass): a 10-deep pass of at
+    most 192 MiB stores through the caches (vk_stencil_ps10.hip), CP = 2."""
     if mode == 'fma' and variant >= 20 and depth <= 11:
         if variant == 30 and depth in (9, 10):
             return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 4>' % depth
+        if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
+            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
         return 'vk_ps::k_diffuse_ps<%d, 4, 2, true>' % depth
     if mode == 'fma' and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
@@ -727,7 +731,7 @@ def main():
                         valu = {'insts_per_launch': rec['valu_insts_per_launch'], 'clock_ghz': rec['clock_ghz'],
                                 'issue_bound_ms': issue_s * 1e3, 'frac': issue_s / (launch_ms * 1e-3),
                                 'busy_counter': rec.get('valu_busy_per_simd')}
-            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode)
+            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode, bytes_per_launch)
             roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
                         'traffic': traffic, 'traffic_from': traffic_from, 'bytes_per_launch': bytes_per_launch,

@@ -1,4 +1,4 @@
-"""Host logic of bench.py that needs no GPU: the untimed settle-step count."""
+"""Host logic of bench.py that needs no GPU: the untimed settle-step count, the pass kernel names."""
 import os
 import sys
 
@@ -21,3 +21,15 @@ def test_settle_steps_disabled_and_capped():
     # microsecond steps (C2 issued eagerly) stop at the cap
     assert bench.settle_steps_needed(3e-6, 3, 30.0) == 2000
     assert bench.settle_steps_needed(3e-6, 3, 30.0, cap=500) == 500
+
+
+def test_stencil_kernel_names_follow_the_launch_rules():
+    """The rocprof names the bench looks its pass up by: the 4096^2 x 2 pass (537 MB)
+    streams its stores, a 10-deep pass of <= 192 MiB (C3's 1024^2 x 2) stores
+    through the caches (vk_stencil_ps10.hip), variant 30 is the vector ring."""
+    whole = 16 * 4096 * 4096 * 2
+    assert bench.stencil_kernel_name(20, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true>'
+    assert bench.stencil_kernel_name(20, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
+    assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true>'
+    assert bench.stencil_kernel_name(30, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 4>'
+    assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
