@@ -47,8 +47,27 @@ def make_halo_exchange(lat, rank: int, world: int, group=None):
         raise ValueError('halo (%d) deeper than the band (%d rows)' % (h, owned))
     nf, ny = len(lat.molecules), lat.ny
     dev = lat.fields.device
-    buf_dev = torch.device('cpu') if _host_staged(dev, group) else dev
-    bufs = {k: torch.empty((nf, h, ny), dtype=torch.float64, device=buf_dev)
+    if not _host_staged(dev, group):
+        # RCCL (or gloo on host planes): each plane's boundary rows are one contiguous
+        # block of the [n_fields, rows_local, ny] buffer, so they are sent from and
+        # received into the buffer itself -- no staging copies around the transfer
+        # (six copy launches per exchange).  Per neighbour the planes go in plane order
+        # on both sides, which is how the point-to-point pairs match.
+        def exchange_direct(src, cnt):
+            ops = []
+            for f in range(nf):
+                if not lat.edge_top:      # neighbour rank-1 owns the rows above
+                    ops.append(dist.P2POp(dist.isend, src[f, lat.row_lo:lat.row_lo + h], rank - 1, group))
+                    ops.append(dist.P2POp(dist.irecv, src[f, lat.row_lo - h:lat.row_lo], rank - 1, group))
+                if not lat.edge_bot:
+                    ops.append(dist.P2POp(dist.isend, src[f, lat.row_hi - h:lat.row_hi], rank + 1, group))
+                    ops.append(dist.P2POp(dist.irecv, src[f, lat.row_hi:lat.row_hi + h], rank + 1, group))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+
+        return exchange_direct
+    bufs = {k: torch.empty((nf, h, ny), dtype=torch.float64, device=torch.device('cpu'))
             for k in ('send_up', 'send_dn', 'recv_up', 'recv_dn')}
 
     def exchange(src, cnt):
