@@ -76,6 +76,22 @@ def _set(current, new, states):
     return new
 
 
+class _EngineCache(tuple):
+    """An engine's per-process cache entry, kept in the process's ``__dict__``
+    (one attribute read per use).  It holds store nodes and the engine itself,
+    so copies and pickles of the process leave it out (None: rebuilt on use)."""
+    __slots__ = ()
+
+    def __copy__(self):
+        return None
+
+    def __deepcopy__(self, memo):
+        return None
+
+    def __reduce__(self):
+        return (type(None), ())
+
+
 class _InvokeNow:
     def __init__(self, process, interval, states):
         self.update = process.next_update(interval, states)
@@ -224,7 +240,7 @@ class Experiment:
             for port in self._port_names(proc):
                 e = self._port_node(path, port)
                 nodes.append((port, e[1], e[3]))
-            ent = (self, path, self._version, nodes)
+            ent = _EngineCache((self, path, self._version, nodes))
             if pd is not None:
                 pd['_engine_state_nodes'] = ent
             else:
@@ -473,7 +489,7 @@ class Experiment:
             plan = (dyn, flux, fields, exch, states, site)
         except (LookupError, KeyError, TypeError):
             plan = None
-        ent = (self._version, process, plan, self, proc_path)
+        ent = _EngineCache((self._version, process, plan, self, proc_path))
         if pd is not None:
             pd['_engine_kinetics_plan'] = ent
         else:

@@ -266,3 +266,31 @@ def test_leaf_columns_apply_equals_update_dict():
         states.append(exp.state)
     assert states[0] == states[1]
     assert 'absent' not in states[0]['agents']['a0']['boundary']['external']
+
+
+def test_engine_caches_stay_out_of_process_copies():
+    """The engine keeps per-process caches (store nodes, kinetics plans) in the
+    process's __dict__; a deep copy or pickle of the process after a run carries
+    None there, not the engine and its store (a shallow copy shares the entries,
+    which check the process and its path before use)."""
+    import copy
+    import pickle
+    from lens_amd.process import BatchedConvenienceKinetics
+    cfg = configs.glc_lct_config()
+    proc = BatchedConvenienceKinetics(dict(cfg, time_step=1.0))
+    topo = {'internal': ('internal',), 'external': ('boundary', 'external'), 'fluxes': ('fluxes',),
+            'fields': ('fields',), 'dimensions': ('dimensions',), 'global': ('boundary',)}
+    init = {'internal': dict(cfg['initial_state']['internal']), 'fluxes': {},
+            'boundary': {'location': [0.5, 0.5], 'mmol_to_counts': 1e6,
+                         'external': dict(cfg['initial_state']['external'])},
+            'dimensions': {'bounds': [2.0, 2.0], 'n_bins': [2, 2], 'depth': 1.0},
+            'fields': {m: np.ones((2, 2)) for m in cfg['initial_state']['external']}}
+    exp = Experiment({'processes': {'k': proc}, 'topology': {'k': topo}, 'initial_state': init,
+                      'invoke': _FakeKineticsInvoke(True)})
+    exp.update(2.0)
+    assert proc.__dict__.get('_engine_state_nodes') is not None
+    assert proc.__dict__.get('_engine_kinetics_plan') is not None
+    for other in (copy.deepcopy(proc), pickle.loads(pickle.dumps(proc))):
+        assert other.__dict__.get('_engine_state_nodes') is None
+        assert other.__dict__.get('_engine_kinetics_plan') is None
+        assert other.signature == proc.signature
