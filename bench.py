@@ -76,6 +76,8 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
         return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
     if mode == 'fma' and depth == 10:
         return 'vk_nt::k_diffuse_wl<10, 3, false, true>'
+    if depth == 10:    # the exact mode's 10-deep whole-step plan
+        return 'vk_nt::k_diffuse_wl<10, 3, false>'
     if variant in (6, 20, 30) and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false>' % depth
     return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 if variant == 2 else 6)

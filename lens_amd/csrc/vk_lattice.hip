@@ -226,11 +226,13 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
     const int bot_reflect = edge_bot ? hi_max - 1 : 0x7fffffff;
     hipStream_t s = (hipStream_t)stream;
     const int last_in_call = sub_begin + sub_count - 1;
-    if (g_stencil_depth == 10 && g_stencil_mode == 1 && sub_count % 10 == 0 && work1) {
-        // Tolerance mode, a block of 10 k substeps: k passes of 10.  The final pass
-        // writes the field without reading it back (no f0), so when the block ends the
-        // step the field is a third buffer (its step-start values are not needed once
-        // the first pass has read them).  The block starts in the buffer the odd-depth
+    if (g_stencil_depth == 10 && sub_count % 10 == 0 && work1) {
+        // A block of 10 k substeps: k passes of 10.  In the tolerance mode the final
+        // pass writes the field without reading it back (no f0), so when the block ends
+        // the step the field is a third buffer (its step-start values are not needed
+        // once the first pass has read them).  The exact mode's final pass re-reads the
+        // step-start field (f0 + (f - f0), in place like the odd-depth plan's), so there
+        // the field is never scratch.  The block starts in the buffer the odd-depth
         // convention holds the state in (field for substep 0, else work[(j-1)&1]) and
         // ends in the one it expects after the block (field after the last substep,
         // else work[last & 1]), so halo exchanges between blocks (row bands) see the
@@ -244,7 +246,8 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         double *S = sub_begin == 0 ? field : work[(sub_begin - 1) & 1];
         double *T = ends_step ? field : work[last_in_call & 1];
         double *cand[3] = {work0, work1, field};
-        const int nc = ends_step ? 3 : 2;    // the field is scratch only in a block that ends the step
+        // the field is scratch only in a tolerance-mode block that ends the step
+        const int nc = (ends_step && g_stencil_mode == 1) ? 3 : 2;
         double *dsts[64];
         bool ok = P >= 1 && P <= 64;
         for (int p = P - 1; ok && p >= 0; --p) {
@@ -265,7 +268,8 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
                 const int lo = max(lo_min, row_lo - grow);
                 const int hi = min(hi_max, row_hi + grow);
                 const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
-                launch_pass(10, s, p ? dsts[p - 1] : S, dsts[p], nullptr, n_fields, field_stride, ny, lo, hi, in_lo,
+                const double *f0 = (g_stencil_mode != 1 && ends_step && p == P - 1) ? field : nullptr;
+                launch_pass(10, s, p ? dsts[p - 1] : S, dsts[p], f0, n_fields, field_stride, ny, lo, hi, in_lo,
                             in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr);
                 int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
                 if (rc) return rc;

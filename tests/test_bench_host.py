@@ -33,3 +33,4 @@ def test_stencil_kernel_names_follow_the_launch_rules():
     assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true>'
     assert bench.stencil_kernel_name(30, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 4>'
     assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
+    assert bench.stencil_kernel_name(6, 10, 'exact') == 'vk_nt::k_diffuse_wl<10, 3, false>'

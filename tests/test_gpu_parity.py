@@ -375,7 +375,8 @@ def test_dopri5_wave_equals_lane_variant_small_network(dev):
 
 
 @pytest.mark.parametrize('variant,depth', [(2, 1), (2, 3), (2, 5), (2, 9), (2, 13), (2, 15), (3, 7), (3, 9),
-                                           (3, 11), (6, 5), (6, 7), (6, 9), (6, 11), (6, 15), (20, 9), (20, 3)])
+                                           (3, 11), (6, 5), (6, 7), (6, 9), (6, 10), (6, 11), (6, 15), (20, 9), (20, 3),
+                                           (20, 10)])
 def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
     """Every kernel variant and temporal-blocking depth reproduces
     scipy.ndimage.convolve bit for bit."""
@@ -401,7 +402,7 @@ def test_stencil_bitwise_vs_scipy_convolve(dev, variant, depth):
 
 @pytest.mark.parametrize('variant,depth,rows', [(2, 9, 64), (2, 7, 128), (2, 11, 32), (2, 15, 256), (3, 9, 64),
                                                 (3, 13, 48), (6, 9, 64), (6, 11, 48), (6, 7, 40), (6, 9, 17),
-                                                (6, 9, 8), (20, 9, 34)])
+                                                (6, 9, 8), (20, 9, 34), (6, 10, 34), (6, 10, 17), (6, 10, 64)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517)])
 def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
     """Multi-tile / multi-chunk geometry: interior tiles, ragged last tile and
@@ -515,20 +516,28 @@ def test_banded_diffusion_equals_whole(dev):
         assert np.array_equal(got, whole.owned('a').cpu().numpy()), (world, halo)
 
 
-def test_banded_depth10_plan_equals_whole(dev):
-    """The tolerance mode's 10-deep whole-step plan on row bands with one
-    100-deep halo block per step (the C4 bench at N > 1) equals the whole plane
-    under the same plan bit for bit: the same cells, the same arithmetic."""
+@pytest.mark.parametrize('mode', ['fma', 'exact'])
+def test_banded_depth10_plan_equals_whole(dev, mode):
+    """The 10-deep block plan on row bands with one 100-deep halo block per step
+    (the C4 bench at N > 1) equals the whole plane under the same plan bit for
+    bit: the same cells, the same arithmetic.  In the exact mode every plan gives
+    scipy's bits, so the whole plane also equals the depth-9 odd plan's."""
     from lens_amd import native
     from lens_amd.distributed import row_bands
     from lens_amd.lattice import Lattice, stencil_depth, stencil_mode
     rng = np.random.default_rng(4)
     nx, ny = 300, 237
     f0 = rng.random((nx, ny)) * 5
-    prev_m, prev_d = stencil_mode('fma'), stencil_depth(10)
+    prev_m, prev_d = stencil_mode(mode), stencil_depth(10)
     try:
         whole = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
         whole.diffuse(1.0)
+        if mode == 'exact':
+            stencil_depth(9)
+            nine = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+            nine.diffuse(1.0)
+            stencil_depth(10)
+            assert np.array_equal(nine.owned('a').cpu().numpy(), whole.owned('a').cpu().numpy())
         for world in (2, 3):
             bands = row_bands(nx, world)
             lats = [Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
@@ -554,7 +563,7 @@ def test_banded_depth10_plan_equals_whole(dev):
         # a block inside the step starts and ends in the same work buffer, so it
         # needs an even number of passes -- halo 30 would plan its middle blocks at
         # odd depths, within the tolerance but not bit for bit)
-        for world, halo in ((3, 50), (3, 20), (2, 40)):
+        for world, halo in ((3, 50), (3, 20), (2, 40)) + (((3, 30),) if mode == 'exact' else ()):
             bands = row_bands(nx, world)
             lats = [Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
                             row_band=b, halo=halo, initial={'a': f0}) for b in bands]
