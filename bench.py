@@ -148,7 +148,9 @@ def stencil_settings(args, world):
         # halo (KH = 10)
         # (row bands too: a middle rank's step at N = 2 / 4 / 8 runs 0.968 / 0.610 / 0.432 ms
         # against 0.995 / 0.628 / 0.450 at depth 9, profiles/r03/r03x_rank_emulate.log)
-        depth = 10 if (args.workload == 'c4' and args.stencil_mode == 'fma') else 9
+        # (exact mode too since round 4: 1.830 / 1.850 / 1.827 against 1.873 / 1.867 / 1.908 ms
+        # per C4 step at depth 9, profiles/r04/r04af/)
+        depth = 10 if args.workload == 'c4' else 9
     rows = args.stencil_rows
     if rows is None:
         # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of
@@ -600,8 +602,7 @@ def main():
     exact_pass_ms = None
     if lat is not None and args.stencil_mode != 'exact':
         stencil_mode('exact')             # the bit-exact pass on the same planes, for comparison
-        # (the exact mode has no 10-deep plan: its 9-deep pass)
-        exact_pass_ms = time_stencil_pass(lat, 9 if args.stencil_depth == 10 else args.stencil_depth)
+        exact_pass_ms = time_stencil_pass(lat, args.stencil_depth)
         stencil_mode(args.stencil_mode)
     copy_floor = time_copy_floor(lat) if lat is not None and world == 1 else None
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)

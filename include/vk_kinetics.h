@@ -242,11 +242,13 @@ int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fi
                        double binvol_avogadro, vk_stream_t stream);
 
 /* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
- * 1..15; 1 = one launch per substep; default 9; or 10: a tolerance-mode whole
- * step of a multiple of 10 substeps as 10-deep passes over three buffers).
- * Each call is planned as the fewest odd-depth passes <= k, as even as
- * possible.  Returns the previous value; other k only query.  Exact mode:
- * bit-identical for every depth.                                           */
+ * 1..15; 1 = one launch per substep; or 10, the default: a block of a multiple
+ * of 10 substeps as 10-deep passes -- in the tolerance mode over three buffers
+ * when the block ends the step, in the exact mode with the final pass re-reading
+ * the step-start field -- and every other call at depth 9).  Odd depths plan
+ * each call as the fewest odd-depth passes <= k, as even as possible.  Returns
+ * the previous value; other k only query.  Exact mode: bit-identical for every
+ * depth.                                                                    */
 int vk_set_stencil_depth(int32_t k);
 
 /* Fused-pass kernel variant.  Exact mode: 2 / 3 = wave tile with DPP lane

@@ -113,7 +113,7 @@ extern "C" int vk_set_stencil_mode(int32_t mode) {
 // tolerance-mode whole step of a multiple of 10 substeps as 10-deep passes (three
 // buffers: the field itself is free once the first pass has read it), other calls
 // as depth 9
-static int g_stencil_depth = 9;
+static int g_stencil_depth = 10;   // 10-deep block plan (odd-depth plan at 9 for other counts)
 
 extern "C" int vk_set_stencil_depth(int32_t k) {
     const int prev = g_stencil_depth;

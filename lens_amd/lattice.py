@@ -39,7 +39,7 @@ def stencil_depth(k: int = 0) -> int:
     """Set (1..15 odd, or 10) / query (0) the substeps fused per HBM pass; returns the previous.
     10 plans a block of a multiple of 10 substeps as 10-deep passes (vk_diffuse; in the
     exact mode the last one re-reads the step-start field, as the odd-depth plan's
-    final pass does); every other call then runs at depth 9."""
+    final pass does); every other call then runs at depth 9.  The default is 10."""
     native.load()
     return native._lib.vk_set_stencil_depth(int(k))
 
