@@ -101,19 +101,26 @@ def run_batch(calls, device=None) -> List[dict]:
 
 
 class _Future:
-    def __init__(self, owner, slot):
+    """One recorded call's result: filled in by the owner's flush (the first
+    ``get()`` / ``raw()`` of the step launches every recorded call)."""
+    __slots__ = ('owner', 'result')
+
+    def __init__(self, owner):
         self.owner = owner
-        self.slot = slot
+        self.result = None
 
     def get(self, timeout=0):
         """The reference's update dict (convenience_kinetics.py:316-349)."""
-        return self.owner._result(self.slot)
+        process, f, d, c = self.raw()
+        return process.unpack_update(f, d, c)
 
     def raw(self):
         """(process, fluxes, deltas, counts) -- the same outputs before they are
         packed into the update dict; lens_amd.engine.Experiment applies them
         straight into the store (same updaters, same order)."""
-        return self.owner._raw(self.slot)
+        if self.result is None:
+            self.owner.flush()
+        return self.result
 
 
 class _Immediate:
@@ -144,8 +151,6 @@ class BatchedInvoke:
     def __init__(self, device=None):
         self.device = device
         self._pending = []
-        self._results = {}
-        self._next = 0
 
     def __call__(self, process, interval, states):
         if not isinstance(process, BatchedConvenienceKinetics):
@@ -153,29 +158,21 @@ class BatchedInvoke:
             if raw is not None:
                 return _ImmediateLeaves(raw(interval, states))
             return _Immediate(process.next_update(interval, states))
-        slot = self._next
-        self._next += 1
-        self._pending.append((slot, _Packed(process, interval, states)))
-        return _Future(self, slot)
+        fut = _Future(self)
+        self._pending.append((fut, _Packed(process, interval, states)))
+        return fut
 
     def flush(self):
+        """Launch every recorded call: one kernel per (network, interval,
+        integrator) group; each future receives its agent's outputs."""
         if not self._pending:
             return
         pending, self._pending = self._pending, []
-        groups: Dict[Tuple, List[Tuple[int, _Packed]]] = {}
-        for slot, it in pending:
+        groups: Dict[Tuple, List[Tuple[_Future, _Packed]]] = {}
+        for fut, it in pending:
             key = (it.process.signature, it.interval, it.process.parameters.get('integrator', 'euler'))
-            groups.setdefault(key, []).append((slot, it))
+            groups.setdefault(key, []).append((fut, it))
         for members in groups.values():
             res = _run_group([it for _, it in members], self.device, raw=True)
-            for (slot, _), r in zip(members, res):
-                self._results[slot] = r
-
-    def _raw(self, slot):
-        if slot not in self._results:
-            self.flush()
-        return self._results.pop(slot)
-
-    def _result(self, slot):
-        process, f, d, c = self._raw(slot)
-        return process.unpack_update(f, d, c)
+            for (fut, _), r in zip(members, res):
+                fut.result = r
