@@ -1,4 +1,4 @@
-// Tolerance-mode fused stencil passes in pair-sum form (variants 20-22; the
+// Tolerance-mode fused stencil passes in pair-sum form (variant 20 and its vector-ring form 30; the
 // tolerance-mode default), instantiated by vk_stencil_ps*.hip.  diffusion_field.py:385-394 advances every cell by
 // f += coef * (N + S + E + W - 4C); the exact mode reproduces scipy's
 // convolve rounding (vk_stencil_kernels.h).  The tolerance mode only has to
@@ -63,9 +63,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *row, in
 // one tile wide, or a reflected row in reach): columns clamped per element and
 // stores masked per column.  Otherwise 16-B buffer accesses: a lane left or
 // right of the plane loads zeros (its columns are halo) and stores nothing.
-// CP (A/B): bit 0 = streaming (nt) loads, bit 1 = plain (cached) stores (0 = plain loads and
-// streaming stores, the default); bit 2 = the stage-0 ring holds each row as one 16-B vector
-// (see PsState)
+// CP: bit 0 = streaming (nt) loads (A/B only), bit 1 = plain (cached) stores -- the 10-deep
+// pass's choice when its planes fit the MALL (vk_stencil_ps10.hip); 0 = plain loads and
+// streaming stores, the default; bit 2 = the stage-0 ring holds each row as one 16-B vector
+// (variant 30, see PsState)
 template <int C, bool CL, int CP = 0>
 __device__ __forceinline__ void ps_load(double (&out)[C], const double *__restrict__ row, const PsLane &L) {
     if constexpr (!CL) {
