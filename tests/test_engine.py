@@ -294,3 +294,41 @@ def test_engine_caches_stay_out_of_process_copies():
         assert other.__dict__.get('_engine_state_nodes') is None
         assert other.__dict__.get('_engine_kinetics_plan') is None
         assert other.signature == proc.signature
+
+
+def test_batched_invoke_groups_and_fills_futures(monkeypatch):
+    """BatchedInvoke on the host side (the launch replaced): calls are grouped by
+    (network, interval, integrator) in first-call order, each group is one
+    _run_group call over its members in call order, every future receives its
+    own agent's outputs, and the first get() / raw() flushes everything recorded."""
+    from lens_amd import invoke as inv
+    from lens_amd.process import BatchedConvenienceKinetics
+    runs = []
+
+    def fake_run_group(items, device=None, raw=False):
+        runs.append([(it.process.tag, it.interval) for it in items])
+        t = items[0].process.table
+        return [(it.process, [float(it.process.tag)] * t.n_reactions, [0.0] * t.n_dyn, [it.process.tag] * t.n_ext)
+                for it in items]
+
+    monkeypatch.setattr(inv, '_run_group', fake_run_group)
+    cfg_a, cfg_b = configs.glc_lct_config(), configs.glc_ac_config()
+    procs = []
+    for tag, (cfg, dt) in enumerate([(cfg_a, 1.0), (cfg_b, 1.0), (cfg_a, 1.0), (cfg_a, 2.0), (cfg_b, 1.0)]):
+        p = BatchedConvenienceKinetics(dict(cfg, time_step=dt))
+        p.tag = tag
+        procs.append((p, dt, cfg))
+    b = inv.BatchedInvoke()
+    futs = []
+    for p, dt, cfg in procs:
+        states = {port: dict(vals) for port, vals in cfg['initial_state'].items()}
+        states['global'] = {'mmol_to_counts': 1e6, 'location': [0.5, 0.5]}
+        futs.append(b(p, dt, states))
+    assert runs == []                                   # nothing launched before the first result is asked for
+    p3, f3, _, c3 = futs[3].raw()
+    assert p3 is procs[3][0] and f3[0] == 3.0 and c3[0] == 3
+    assert runs == [[(0, 1.0), (2, 1.0)], [(1, 1.0), (4, 1.0)], [(3, 2.0)]]
+    for k, fut in enumerate(futs):                      # the rest are already filled: no second launch
+        assert fut.raw()[0] is procs[k][0] and fut.raw()[3][0] == k
+        assert fut.get()['fluxes'] == dict.fromkeys(procs[k][0].table.reaction_ids, float(k))
+    assert len(runs) == 3
