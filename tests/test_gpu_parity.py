@@ -424,6 +424,30 @@ def test_stencil_large_tiles_vs_c_oracle(dev, variant, depth, rows, shape):
     assert np.array_equal(lat.owned('a').cpu().numpy(), ref)
 
 
+@pytest.mark.parametrize('dt', [0.095, 0.2, 0.3, 1.1, 0.55, 0.1])
+def test_exact_depth10_block_counts_vs_c_oracle(dev, dt):
+    """The exact mode's 10-deep plan for every block shape a step can have: 10
+    substeps (dt 0.095: one pass would run in place, so the odd-depth plan takes
+    it), 20 / 30 / 110 (10-deep passes, the last one re-reading the step-start
+    field) and 55 / 11 (dt 0.55 / 0.1: not multiples of 10, odd depths) -- bit for
+    bit against the C oracle."""
+    from lens_amd.lattice import Lattice, n_substeps, stencil_depth, stencil_kernel
+    rng = np.random.default_rng(21)
+    nx, ny = 333, 517
+    f0 = rng.random((nx, ny))
+    prev_d, prev_k = stencil_depth(10), stencil_kernel(6, 34)
+    try:
+        lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+        n_sub = lat.diffuse(dt)
+    finally:
+        stencil_depth(prev_d)
+        stencil_kernel(prev_k, 0)
+    assert n_sub == n_substeps(dt, 0.01)
+    ref = np.ascontiguousarray(f0.copy())
+    cpu.diffuse(ref, 5.0 * 0.01, n_sub)
+    assert np.array_equal(lat.owned('a').cpu().numpy(), ref)
+
+
 def test_uniform_summary(dev):
     """vk_field_uniform: (v, v) for a one-valued plane, (-inf, inf) otherwise --
     including a single differing cell at the very end and a NaN plane."""
