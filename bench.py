@@ -22,13 +22,81 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-
 REPO = os.path.dirname(os.path.abspath(__file__))
+
+
+def _gpus_flag(argv):
+    """The value of --gpus in `argv` (1 if absent), without the full parser."""
+    p = argparse.ArgumentParser(add_help=False)
+    p.add_argument('--gpus', type=int, default=1)
+    return p.parse_known_args(argv)[0].gpus
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def rank_launch_command(argv, n, port):
+    """The child command that runs `bench.py <argv>` as n ranks, one per GPU."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(n),
+            '--master-addr', '127.0.0.1', '--master-port', str(port),
+            os.path.join(REPO, 'bench.py')] + list(argv)
+
+
+def launch_ranks(argv, environ=None, popen=subprocess.Popen):
+    """Make `--gpus N` mean N ranks.  Runs before anything touches the GPU.
+
+    - WORLD_SIZE unset and N > 1: start torch.distributed.run with N ranks as a
+      CHILD process (never an exec: on this pool a process that initialised
+      the GPU must not be replaced), wait for it, and return its exit code.
+    - WORLD_SIZE set and different from N: exit non-zero (a launcher with a
+      different rank count than the run claims).
+    - Otherwise return None: this process is a rank (or the only one).
+
+    Replaces the reference's parallel dispatch of agent processes
+    (/root/reference/vivarium/core/experiment.py:1171-1178) at the job level:
+    one process per GPU."""
+    environ = os.environ if environ is None else environ
+    n = _gpus_flag(argv)
+    if n < 1:
+        raise SystemExit('bench.py: --gpus must be >= 1 (got %d)' % n)
+    world = environ.get('WORLD_SIZE')
+    if world is not None:
+        if int(world) != n:
+            raise SystemExit('bench.py: --gpus %d but WORLD_SIZE=%s: the launcher started a different number '
+                             'of ranks than the run reports' % (n, world))
+        return None
+    if n == 1:
+        return None
+    child = popen(rank_launch_command(argv, n, _free_port()))
+
+    def forward(signum, _frame):
+        child.send_signal(signum)
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        return child.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
+if __name__ == '__main__':
+    # before lens_amd (which loads the HIP library) and before any torch.cuda call
+    _rc = launch_ranks(sys.argv[1:])
+    if _rc is not None:
+        sys.exit(_rc)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
 sys.path.insert(0, REPO)
 
 from lens_amd import configs  # noqa: E402
@@ -63,15 +131,17 @@ SPLIT_STEPS = 6            # eager steps timed for the kinetics / diffusion spli
 
 
 def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
-    """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse).
-    ``pass_bytes`` (source + destination rows of one pass): a 10-deep pass of at
-    most 192 MiB stores through the caches (vk_stencil_ps10.hip), CP = 2."""
-    if mode == 'fma' and variant >= 20 and depth <= 11:
+    """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse):
+    the full template argument list, as rocprofv3 prints it.  ``pass_bytes``
+    (source + destination rows of one pass): a 10-deep pass of at most 192 MiB
+    stores through the caches (vk_stencil_ps10.hip), CP = 2."""
+    if mode == 'fma' and variant >= 20 and depth <= 11 and (depth % 2 == 1 or depth == 10):
+        # k_diffuse_ps<K, PD, C, SC, CP> (vk_stencil_ps.h); SC = the rescaled form (coef not ~1/4)
         if variant == 30 and depth in (9, 10):
             return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 4>' % depth
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
             return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
-        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true>' % depth
+        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0>' % depth
     if mode == 'fma' and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
     if mode == 'fma' and depth == 10:
@@ -100,10 +170,10 @@ def parse(argv=None):
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=20,
-                   help='tolerance mode: 20 = pair-sum passes (default), 21 / 22 = 2 / 6 rows prefetched, '
-                        '6 = the variant-6 FMA form; exact mode: 2 / 3 = wave tiles prefetching 3 / 6 rows, '
-                        '6 (and 20-22) = 3 with streaming stores')
+    p.add_argument('--stencil-kernel', type=int, default=20, choices=[2, 3, 6, 20, 30],
+                   help='tolerance mode: 20 = pair-sum passes (default), 30 = pair-sum with the stage-0 ring '
+                        'held as 16-B vectors, 6 = the variant-6 FMA form; exact mode: 2 / 3 = wave tiles '
+                        'prefetching 3 / 6 rows, 6 (and 20, 30) = 3 with streaming stores')
     p.add_argument('--stencil-depth', type=int, default=None,
                    help='substeps fused per HBM pass (odd, or 10: tolerance-mode whole steps as 10-deep passes); '
                         'default 10 for C4 in the fma mode, else 9')
@@ -716,15 +786,20 @@ def main():
             bytes_per_launch = 16.0 * cells          # algorithmic: read + write each cell once
             achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
             traffic = valu = traffic_from = None
+            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode, bytes_per_launch)
             import glob
             for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_stencil*.json'))) if world == 1 else []:
                 with open(pmc) as f:
                     rec = json.load(f)
-                # the committed PMC pass must describe this exact launch geometry and mode
+                # the committed PMC pass must describe this exact launch geometry and mode, and
+                # name the kernel this run launches (rocprof's full template name): a record
+                # of an older kernel build is refused
                 if (rec.get('depth'), rec.get('rows'), rec.get('cells'), rec.get('variant'),
-                        rec.get('mode', 'exact')) == (depth, args.stencil_rows, cells, args.stencil_kernel,
-                                                      args.stencil_mode):
-                    traffic_from = os.path.relpath(pmc, REPO)
+                        rec.get('mode', 'exact'), rec.get('kernel')) == (depth, args.stencil_rows, cells,
+                                                                         args.stencil_kernel, args.stencil_mode,
+                                                                         kname):
+                    traffic_from = os.path.relpath(pmc, REPO) + (' (commit %s)' % rec['commit']
+                                                                 if rec.get('commit') else '')
                     traffic = rec.get('hbm_bytes_per_launch')
                     if rec.get('valu_insts_per_launch') and rec.get('clock_ghz'):
                         # the pass against the VALU-issue bound: one wave64 VALU instruction
@@ -734,7 +809,6 @@ def main():
                         valu = {'insts_per_launch': rec['valu_insts_per_launch'], 'clock_ghz': rec['clock_ghz'],
                                 'issue_bound_ms': issue_s * 1e3, 'frac': issue_s / (launch_ms * 1e-3),
                                 'busy_counter': rec.get('valu_busy_per_simd')}
-            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode, bytes_per_launch)
             roofline = {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                         'peak': HBM_PEAK_GBPS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBPS,
                         'traffic': traffic, 'traffic_from': traffic_from, 'bytes_per_launch': bytes_per_launch,

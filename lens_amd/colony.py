@@ -616,7 +616,13 @@ class Colony:
                         native.ptr(stamps), 3 * k + tag, native.stream_handle()), 'vk_timestamp'))
                 self.step(dt, stamp=stamp)
         self.time, self.step_index = t0, s0      # capture ran nothing
-        self.counts = counts0
+        if spl > 1:
+            # step_many pointed flux / counts / nsteps at the last step's rows of the
+            # step buffers, which is where every replay leaves them
+            self.flux, self.counts, self.nsteps = (self.flux_steps[spl - 1], self.counts_steps[spl - 1],
+                                                   self.nsteps_steps[spl - 1])
+        else:
+            self.counts = counts0
 
         def replay():
             # the graph holds raw device pointers and the agent count of capture time

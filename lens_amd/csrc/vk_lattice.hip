@@ -163,8 +163,10 @@ __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ sr
 static void launch_pass(int k, hipStream_t s, const double *src, double *dst, const double *f0, int nf, int64_t fs,
                         int ny, int lo, int hi, int in_lo, int in_hi, int top, int bot, double coef, const double *mm,
                         const VkPsCouple *cp) {
-    if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11) {
-        // tolerance mode, pair-sum passes (the final pass writes the new field as is)
+    if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11 && ((k & 1) || k == 10)) {
+        // tolerance mode, pair-sum passes (the final pass writes the new field as is);
+        // they are instantiated for k = 3, 5, 7, 9, 10, 11 (an even k < 10 takes the
+        // wave tiles below)
         vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
     } else if (k == 10 ||
                ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11))) {

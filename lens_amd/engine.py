@@ -100,6 +100,52 @@ class _InvokeNow:
         return self.update
 
 
+_END = object()          # _PathIndex: marks a path's own entry in the trie
+
+
+class _PathIndex:
+    """The store / process paths the engine's caches hold entries for, as a trie, so
+    that deleting a subtree drops exactly its entries in time proportional to the
+    subtree (the reference drops them with the deleted Store objects,
+    experiment.py:505-509).  Each path carries a set of tags (e.g. its ports)."""
+    __slots__ = ('root',)
+
+    def __init__(self):
+        self.root = {}
+
+    def add(self, path, tag=None):
+        node = self.root
+        for k in path:
+            nxt = node.get(k)
+            if nxt is None:
+                nxt = node[k] = {}
+            node = nxt
+        tags = node.get(_END)
+        if tags is None:
+            tags = node[_END] = set()
+        tags.add(tag)
+
+    def pop_prefix(self, prefix):
+        """Remove and return [(path, tags)] of every path under `prefix` (itself included)."""
+        node = self.root
+        for k in prefix[:-1]:
+            node = node.get(k)
+            if node is None:
+                return []
+        sub = node.pop(prefix[-1], None) if prefix else node
+        if not prefix:
+            self.root = {}
+        out, stack = [], ([(tuple(prefix), sub)] if sub else [])
+        while stack:
+            p, n = stack.pop()
+            for k, v in n.items():
+                if k is _END:
+                    out.append((p, v))
+                else:
+                    stack.append((p + (k,), v))
+        return out
+
+
 class Experiment:
     def __init__(self, config):
         self.processes = config['processes']
@@ -126,6 +172,8 @@ class Experiment:
         self._plans: Dict[Tuple, Tuple] = {}        # process path -> (version, process, kinetics plan)
         self._state_nodes: Dict[Tuple, Tuple] = {}  # process path -> (version, process, [(port, parent, key)])
         self._version = 0
+        self._proc_index = _PathIndex()            # process paths with cached port entries (tag: port)
+        self._schema_index = _PathIndex()          # store paths with a schema updater / divider
         self.dividers: Dict[Tuple, object] = {}   # store path (with '*' globs) -> schema _divider
         self._div_globs: List[Tuple] = []
         self._structure = 0                        # moves when processes join or leave the tree
@@ -160,12 +208,27 @@ class Experiment:
         p = self._port_paths.get(key)
         if p is None:
             p = self._port_paths[key] = normalize_path(proc_path[:-1] + tuple(self._topology_of(proc_path)[port]))
+            self._proc_index.add(proc_path, port)
         return p
 
     def get(self, path):
         v = self.state
         for key in path:
             v = v[key]
+        return v
+
+    def _lookup(self, path):
+        """The node at `path`, or None when a segment is missing: Store.apply_update
+        descends only into keys its `inner` holds and drops the rest of an update
+        (experiment.py:698-711), e.g. an update to an agent that an earlier update of
+        the same batch deleted or divided."""
+        v = self.state
+        for key in path:
+            if not isinstance(v, dict):
+                return None
+            v = v.get(key, _MISSING)
+            if v is _MISSING:
+                return None
         return v
 
     def _register(self, path, schema):
@@ -175,6 +238,8 @@ class Experiment:
         self._clear_leaf_caches()
         keys = [k for k in schema if not k.startswith('_')]
         if ('_default' in schema or '_value' in schema or '_updater' in schema or '_divider' in schema) and not keys:
+            if '_updater' in schema or '_divider' in schema:
+                self._schema_index.add(path)
             if '_updater' in schema:           # a schema without one keeps the store's updater
                 self.schema.setdefault(path, schema['_updater'])
                 if '*' in path and path not in self._globs:
@@ -226,7 +291,10 @@ class Experiment:
         ent = self._port_nodes.get(key)
         if ent is None or ent[0] != self._version:
             path = self.port_path(proc_path, port)
-            ent = self._port_nodes[key] = (self._version, self.get(path[:-1]), path[:-1], path[-1])
+            parent = self._lookup(path[:-1])
+            ent = self._port_nodes[key] = (self._version, parent if isinstance(parent, dict) else None,
+                                           path[:-1], path[-1])
+            self._proc_index.add(proc_path, port)
         return ent
 
     def process_states(self, path, proc):
@@ -245,11 +313,17 @@ class Experiment:
                 pd['_engine_state_nodes'] = ent
             else:
                 self._state_nodes[path] = ent
-        return {port: parent[key] for port, parent, key in ent[3]}
+        try:
+            return {port: parent[key] for port, parent, key in ent[3]}
+        except TypeError:
+            missing = [port for port, parent, _ in ent[3] if parent is None]
+            raise KeyError('process %s: no store for port(s) %s' % (path, missing)) from None
 
     def apply_update(self, update, proc_path):
         for port, value in update.items():
             _, parent, ppath, key = self._port_node(proc_path, port)
+            if parent is None:          # the port's store is gone (deleted earlier in this batch)
+                continue
             self._apply(parent, ppath, key, value, proc_path)
 
     def _apply(self, parent, ppath, key, update, proc_path):
@@ -293,7 +367,7 @@ class Experiment:
                 states = {}
                 for up, pp in mapping.items():
                     ent = self._port_node(proc_path, pp)
-                    states[up] = ent[1][ent[3]]
+                    states[up] = ent[1].get(ent[3]) if ent[1] is not None else None
         else:
             names = self._leaf_updaters.get(ppath)
             if names is None:
@@ -392,7 +466,27 @@ class Experiment:
             for _, proc in (self._walk(lost, ()) if isinstance(lost, dict) else [((), lost)]):
                 self._deleted[id(proc)] = proc
                 self._ports.pop(id(proc), None)
+        self._forget(path)
         self._structure_changed()
+
+    def _forget(self, path):
+        """Drop every cache entry under a deleted path: the port nodes and port paths
+        of its processes (a port node holds its parent store node, i.e. the deleted
+        subtree, alive), and the schema updaters and dividers registered under it, so
+        that a path generated again later takes its new processes' topology and schema."""
+        for ppath, ports in self._proc_index.pop_prefix(path):
+            for port in ports:
+                self._port_nodes.pop((ppath, port), None)
+                self._port_paths.pop((ppath, port), None)
+            self._state_nodes.pop(ppath, None)
+            self._plans.pop(ppath, None)
+        for spath, _ in self._schema_index.pop_prefix(path):
+            self.schema.pop(spath, None)
+            self.dividers.pop(spath, None)
+            if spath in self._globs:
+                self._globs.remove(spath)
+            if spath in self._div_globs:
+                self._div_globs.remove(spath)
 
     def _divider_at(self, path):
         if path in self.dividers:
@@ -450,7 +544,7 @@ class Experiment:
         try:
             def leaves(port, names):
                 _, parent, ppath, key = self._port_node(proc_path, port)
-                node = parent.get(key, _MISSING)
+                node = parent.get(key, _MISSING) if parent is not None else _MISSING
                 if node is _MISSING:
                     return [None] * len(names)           # no such port: apply_update skips it
                 if not isinstance(node, dict):
@@ -471,7 +565,7 @@ class Experiment:
             dyn = [leaves(port, [name])[0] for port, name in t.species[:t.n_dyn]]
             flux = leaves('fluxes', t.reaction_ids)
             _, fparent, fppath, fkey = self._port_node(proc_path, 'fields')
-            fnode = fparent.get(fkey, _MISSING)
+            fnode = fparent.get(fkey, _MISSING) if fparent is not None else _MISSING
             if not isinstance(fnode, dict):
                 raise LookupError                        # the generic path decides
             states = {}
@@ -556,6 +650,8 @@ class Experiment:
         if not up.ids:
             return
         _, parent, ppath, key = self._port_node(proc_path, 'agents')
+        if parent is None:
+            return
         agents = parent.get(key, _MISSING)
         if not isinstance(agents, dict):
             self.apply_update(up.as_dict(), proc_path)

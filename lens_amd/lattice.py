@@ -49,10 +49,18 @@ def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
     returns the previous variant.  Exact mode: 2 / 3 = lag-1 wave tiles with 3 / 6
     rows prefetched, 6 = 3 with streaming stores (the exact mode's default kernel).
     Tolerance mode: 20 = pair-sum passes (the default), 30 = the same with the
-    stage-0 ring held as 16-B vectors, 6 = the 4-op FMA wave tiles.  Other numbers
-    are ignored (retired variants)."""
+    stage-0 ring held as 16-B vectors, 6 = the 4-op FMA wave tiles.  Any other
+    number (a retired variant) raises ValueError: the library would
+    keep the previous variant, and a run would time something else than it names."""
     native.load()
+    if int(variant) != -1 and int(variant) not in STENCIL_VARIANTS:
+        raise ValueError('stencil kernel %d is not built (variants: %s)' % (variant, sorted(STENCIL_VARIANTS)))
+    if int(rows) != -1 and not (int(rows) == 0 or 8 <= int(rows) <= 4096):
+        raise ValueError('stencil tile rows must be 0 (auto) or 8..4096, got %d' % rows)
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
+
+
+STENCIL_VARIANTS = frozenset((2, 3, 6, 20, 30))     # vk_set_stencil_kernel (vk_lattice.hip)
 
 
 def stencil_mode(mode=None) -> str:

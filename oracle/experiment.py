@@ -199,10 +199,21 @@ class OracleExperiment:
         for port, value in update.items():
             self._apply(self.port_path(proc_path, port), value, proc_path)
 
+    def _lookup(self, path):
+        node = self.state
+        for key in path:
+            if not isinstance(node, dict) or key not in node:
+                return None
+            node = node[key]
+        return node
+
     def _apply(self, path, update, proc_path):
-        parent = self.get(path[:-1])
-        if path[-1] not in parent:
-            return                                   # Store.apply_update skips unknown keys
+        # Store.apply_update descends only into keys `inner` holds (experiment.py:699-711):
+        # an update below a missing key (e.g. an agent deleted earlier in the same
+        # batch) is dropped
+        parent = self._lookup(path[:-1])
+        if not isinstance(parent, dict) or path[-1] not in parent:
+            return
         current = parent[path[-1]]
         inline = isinstance(update, dict) and '_updater' in update
         if isinstance(current, dict) and not inline:

@@ -2,7 +2,14 @@
 profiles/pmc_stencil.json, which bench.py reads for roofline.traffic.
 
     python scripts/pmc_to_json.py KERNEL CELLS DEPTH ROWS VARIANT fetch.csv write.csv [out.json] [--sq sq.csv]
-                                  [--mode exact|fma]
+                                  [--mode exact|fma] [--commit SHA]
+
+KERNEL is the kernel's full template name as rocprofv3 prints it (e.g.
+'vk_ps::k_diffuse_ps<10, 4, 2, true, 0>'); a dispatch matches only if its name,
+without a leading 'void ' and its argument list, is exactly that.  --commit
+records the tree the counters were taken on (bench.py names it in
+roofline.traffic_from, and refuses a record whose kernel differs from the one
+it launches).
 
 --sq: a pass with SQ_INSTS_VALU and GRBM_GUI_ACTIVE adds the VALU instructions
 per launch and the effective clock (GRBM_GUI_ACTIVE / 8 XCDs / wall), from
@@ -18,11 +25,24 @@ import json
 import sys
 
 
+def base_name(name):
+    """'void ns::k<1, 2>(double const*, int)' -> 'ns::k<1, 2>'"""
+    if name.startswith('void '):
+        name = name[5:]
+    depth = 0
+    for i, ch in enumerate(name):
+        depth += ch == '<'
+        depth -= ch == '>'
+        if ch == '(' and depth == 0:
+            return name[:i].strip()
+    return name.strip()
+
+
 def mean_counter(path, kernel, counter):
     per = {}
     for r in csv.DictReader(open(path)):
         name = r['Kernel_Name']
-        if (name.startswith(kernel) or name.startswith('void ' + kernel)) and r['Counter_Name'] == counter:
+        if base_name(name) == kernel and r['Counter_Name'] == counter:
             per[r['Dispatch_Id']] = per.get(r['Dispatch_Id'], 0.0) + float(r['Counter_Value'])
     if not per:
         raise SystemExit('no %s samples for %s in %s' % (counter, kernel, path))
@@ -39,6 +59,11 @@ if '--mode' in argv:
     i = argv.index('--mode')
     mode = argv[i + 1]
     del argv[i:i + 2]
+commit = None
+if '--commit' in argv:
+    i = argv.index('--commit')
+    commit = argv[i + 1]
+    del argv[i:i + 2]
 sq = None
 if '--sq' in argv:
     i = argv.index('--sq')
@@ -50,7 +75,7 @@ fetch_kib, nf = mean_counter(fcsv, kernel, 'FETCH_SIZE')
 write_kib, nw = mean_counter(wcsv, kernel, 'WRITE_SIZE')
 rec = {
     'kernel': kernel, 'cells': int(cells), 'depth': int(depth), 'rows': int(rows), 'variant': int(variant),
-    'mode': mode,
+    'mode': mode, 'commit': commit,
     'fetch_size_kib': fetch_kib, 'write_size_kib': write_kib, 'dispatches': [nf, nw],
     'read_bytes_per_launch': 2.0 * fetch_kib * 1024.0,
     'write_bytes_per_launch': write_kib * 1024.0,
@@ -62,7 +87,7 @@ if sq:
     per = {}
     for r in csv.DictReader(open(sq)):
         name = r['Kernel_Name']
-        if name.startswith(kernel) or name.startswith('void ' + kernel):
+        if base_name(name) == kernel:
             d = per.setdefault(r['Dispatch_Id'], {'ns': int(r['End_Timestamp']) - int(r['Start_Timestamp'])})
             d[r['Counter_Name']] = d.get(r['Counter_Name'], 0.0) + float(r['Counter_Value'])
     top = max(d['SQ_INSTS_VALU'] for d in per.values())

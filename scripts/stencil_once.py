@@ -11,7 +11,7 @@ lat = Lattice(['glc__D_e', 'ac_e'], (n, n), (float(n), float(n)), 10.0, 5.0, dev
               initial={'glc__D_e': glc, 'ac_e': glc * 0.5})
 stencil_depth(depth)
 from lens_amd.lattice import stencil_kernel
-stencil_kernel(int(os.environ.get('VARIANT', '1')), int(os.environ.get('ROWS', '128')))
+stencil_kernel(int(os.environ.get('VARIANT', '20')), int(os.environ.get('ROWS', '128')))
 from lens_amd.lattice import stencil_mode
 stencil_mode(os.environ.get('MODE', 'exact'))
 for _ in range(reps):

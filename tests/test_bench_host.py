@@ -28,9 +28,76 @@ def test_stencil_kernel_names_follow_the_launch_rules():
     streams its stores, a 10-deep pass of <= 192 MiB (C3's 1024^2 x 2) stores
     through the caches (vk_stencil_ps10.hip), variant 30 is the vector ring."""
     whole = 16 * 4096 * 4096 * 2
-    assert bench.stencil_kernel_name(20, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true>'
+    assert bench.stencil_kernel_name(20, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(20, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
-    assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true>'
+    assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(30, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 4>'
     assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
     assert bench.stencil_kernel_name(6, 10, 'exact') == 'vk_nt::k_diffuse_wl<10, 3, false>'
+
+
+class _FakeChild:
+    def __init__(self, cmd, rc=0):
+        self.cmd, self.rc, self.signals = cmd, rc, []
+
+    def wait(self):
+        return self.rc
+
+    def send_signal(self, s):
+        self.signals.append(s)
+
+
+def test_gpus_n_starts_n_ranks_as_a_child_before_any_gpu_call():
+    """--gpus N without a launcher: torch.distributed.run with N ranks, started as
+    a child process (never an exec), whose exit code the parent returns; nothing
+    before it initialised the GPU."""
+    import torch
+    started = []
+
+    def popen(cmd):
+        assert not torch.cuda.is_initialized()
+        started.append(_FakeChild(cmd, rc=3))
+        return started[-1]
+    argv = ['--gpus', '4', '--steps', '5', '--warmup', '2', '--dist-backend', 'gloo']
+    rc = bench.launch_ranks(argv, environ={}, popen=popen)
+    assert rc == 3 and len(started) == 1
+    cmd = started[0].cmd
+    assert cmd[:3] == [sys.executable, '-m', 'torch.distributed.run']
+    assert cmd[cmd.index('--nproc-per-node') + 1] == '4'
+    assert cmd[cmd.index('--master-addr') + 1] == '127.0.0.1'
+    assert int(cmd[cmd.index('--master-port') + 1]) > 0
+    i = cmd.index(os.path.join(bench.REPO, 'bench.py'))
+    assert cmd[i + 1:] == argv          # the ranks see the same arguments (and WORLD_SIZE = 4)
+    assert not torch.cuda.is_initialized()
+
+
+def test_gpus_flag_inside_a_launcher_or_on_one_gpu_runs_in_process():
+    never = lambda cmd: (_ for _ in ()).throw(AssertionError('no child expected'))
+    assert bench.launch_ranks(['--gpus', '8'], environ={'WORLD_SIZE': '8'}, popen=never) is None
+    assert bench.launch_ranks([], environ={}, popen=never) is None
+    assert bench.launch_ranks(['--gpus', '1'], environ={}, popen=never) is None
+    assert bench.launch_ranks(['--gpus=2'], environ={'WORLD_SIZE': '2'}, popen=never) is None
+
+
+def test_gpus_flag_mismatching_the_launcher_exits_nonzero():
+    import pytest
+    never = lambda cmd: (_ for _ in ()).throw(AssertionError('no child expected'))
+    with pytest.raises(SystemExit) as e:
+        bench.launch_ranks(['--gpus', '8'], environ={'WORLD_SIZE': '2'}, popen=never)
+    assert e.value.code not in (0, None)
+    with pytest.raises(SystemExit) as e:
+        bench.launch_ranks(['--gpus', '0'], environ={}, popen=never)
+    assert e.value.code not in (0, None)
+
+
+def test_bench_script_with_wrong_world_size_fails_before_importing_lens_amd():
+    """The real entry point: a mismatch exits non-zero with the message, and the
+    check runs before lens_amd (and its HIP library) is imported."""
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE='2')
+    p = subprocess.run([sys.executable, '-X', 'importtime', os.path.join(bench.REPO, 'bench.py'), '--gpus', '4'],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0
+    assert 'WORLD_SIZE=2' in p.stderr
+    assert 'lens_amd' not in p.stderr.replace('WORLD_SIZE', '')
+

@@ -129,9 +129,13 @@ def test_divided_values_follow_the_schema_dividers():
     assert exp.processes['agents']['00']['division'].agent_id == '00'
 
 
+@pytest.mark.parametrize('maker_first', [False, True])
 @pytest.mark.parametrize('structure', ['generate', 'delete', 'add'])
-def test_generate_delete_add_updates(structure):
-    """_generate, _delete and _add at a branch, engine vs oracle."""
+def test_generate_delete_add_updates(structure, maker_first):
+    """_generate, _delete and _add at a branch, engine vs oracle.  With the
+    structural process first, its _delete lands before the deleted agent's own
+    updates of the same batch, which Store.apply_update then drops
+    (experiment.py:699-711) instead of failing."""
     class Maker:
         name = 'maker'
 
@@ -160,8 +164,11 @@ def test_generate_delete_add_updates(structure):
         np.random.seed(1)
         random.seed(1)
         p, t, init = colony(3)
-        p['maker'] = Maker()
-        t['maker'] = {'cells': ('agents',)}
+        if maker_first:
+            p, t = {'maker': Maker(), **p}, {'maker': {'cells': ('agents',)}, **t}
+        else:
+            p['maker'] = Maker()
+            t['maker'] = {'cells': ('agents',)}
         return Experiment({'processes': p, 'topology': t, 'initial_state': init}) if kind == 'engine' else \
             OracleExperiment(p, t, init)
 
@@ -198,3 +205,55 @@ def test_deleted_derivers_are_forgotten_after_their_pass():
         exp.state['agents']['0']['boundary']['divide'] = True
         exp.send_updates([])
         assert '0' not in exp.state['agents'] and '00' in exp.state['agents'], kind
+
+
+def test_deleting_agents_forgets_their_cache_entries():
+    """A dividing colony must not keep every deleted mother's port nodes (each holds
+    the mother's state subtree), port paths, schema updaters or dividers: after
+    the loop, the caches hold entries for live agents only."""
+    np.random.seed(1)
+    random.seed(1)
+    p, t, init = colony(3)
+    exp = Experiment({'processes': p, 'topology': t, 'initial_state': init})
+    for _ in range(12):
+        exp.update(1.0)
+    live = set(exp.state['agents'])
+    assert len(live) > 3                                # the colony divided
+    for (ppath, port) in list(exp._port_nodes) + list(exp._port_paths):
+        if len(ppath) > 1 and ppath[0] == 'agents':
+            assert ppath[1] in live, ppath
+    for path in list(exp.schema) + list(exp.dividers):
+        if len(path) > 1 and path[0] == 'agents' and path[1] != '*':
+            assert path[1] in live, path
+
+
+def test_regenerated_path_takes_its_new_schema():
+    """A path deleted and generated again with another updater uses the new one
+    (the reference builds fresh Stores), not the deleted subtree's."""
+    class Leaf:
+        name = 'leaf'
+
+        def __init__(self, updater):
+            self.updater = updater
+
+        def local_timestep(self):
+            return 1.0
+
+        def is_deriver(self):
+            return False
+
+        def ports_schema(self):
+            return {'x': {'v': {'_default': 0.0, '_updater': self.updater}}}
+
+        def next_update(self, timestep, states):
+            return {'x': {'v': 2.0}}
+
+    exp = Experiment({'processes': {'cells': {'a': {'leaf': Leaf('accumulate')}}},
+                      'topology': {'cells': {'a': {'leaf': {'x': ('x',)}}}},
+                      'initial_state': {'cells': {'a': {'x': {'v': 1.0}}}}})
+    exp.update(1.0)
+    assert exp.state['cells']['a']['x']['v'] == 3.0
+    exp._delete_path(('cells', 'a'))
+    exp._generate(('cells',), ('a',), {'leaf': Leaf('set')}, {'leaf': {'x': ('x',)}}, {'x': {'v': 1.0}})
+    exp.update(1.0)
+    assert exp.state['cells']['a']['x']['v'] == 2.0          # set, not accumulate

@@ -169,6 +169,11 @@ def test_multi_step_launch_equals_single_steps(dev, k):
     replay()
     torch.cuda.synchronize()
     assert torch.equal(c.conc, b.conc) and torch.equal(c.h_state, b.h_state)
+    # after replay the colony's views hold the last replayed step (not the
+    # pre-capture buffers the graph never writes)
+    assert torch.equal(c.flux[:, :c.n], b.flux[:, :b.n])
+    assert torch.equal(c.counts[:, :c.n], b.counts[:, :b.n])
+    assert torch.equal(c.nsteps[:c.n], b.nsteps[:b.n])
     a.check_status()
     c.check_status()
 
