@@ -91,7 +91,9 @@ static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 30) g_stencil_kernel = variant;
+    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 30 ||
+        (variant >= 40 && variant <= 43))
+        g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
 }
@@ -166,7 +168,10 @@ static void launch_pass(int k, hipStream_t s, const double *src, double *dst, co
     if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11 && ((k & 1) || k == 10)) {
         // tolerance mode, pair-sum passes (the final pass writes the new field as is);
         // they are instantiated for k = 3, 5, 7, 9, 10, 11 (an even k < 10 takes the
-        // wave tiles below)
+        // wave tiles below); variants 40-43: the stage-split 10-deep pass
+        if (g_stencil_kernel >= 40 &&
+            vk_launch_sp(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp))
+            return;
         vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
     } else if (k == 10 ||
                ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11))) {
