@@ -14,6 +14,11 @@ bool vk_launch_sp(int variant, VK_STENCIL_LAUNCH_ARGS) {
         case 41: vk_sp::launch<10, 4, 2, 2>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
         case 42: vk_sp::launch<10, 4, 4, 5>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
         case 43: vk_sp::launch<10, 4, 4, 2>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
+        // deeper row prefetch in wave 0 (its iterations are ~5x shorter than a variant-20 wave's)
+        case 44: vk_sp::launch<10, 8, 2, 5>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
+        case 45: vk_sp::launch<10, 12, 2, 5>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
+        case 46: vk_sp::launch<10, 16, 2, 5>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
+        case 47: vk_sp::launch<10, 12, 2, 10>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows); return true;
         default: return false;
     }
 }
