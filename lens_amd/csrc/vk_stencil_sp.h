@@ -76,10 +76,27 @@ __device__ __forceinline__ void xfer_read(double (&v)[C], const __attribute__((a
 typedef __attribute__((address_space(3))) double lds_double;
 
 struct SpXfer {
-    lds_double *in;      // boundary (S-1 -> S): 2 slots of 64 * C doubles (unused by wave 0)
+    lds_double *in;      // boundary (S-1 -> S): slots of 64 * C doubles (unused by wave 0)
     lds_double *out;     // boundary (S -> S+1) (unused by the last wave)
     int lane;
+    // CP bit 3 (flag-synchronised ring, no barrier): per boundary two LDS counters,
+    // [0] rows written by the producer, [1] rows read by the consumer
+    __attribute__((address_space(3))) int *cnt_in, *cnt_out;
+    int seen_in, seen_out;   // last counter values this wave observed (wave-uniform)
+    int is;                  // the chunk's first local iteration (row index of T = 0)
 };
+
+constexpr int SP_FLAGS = 8;          // CP bit: hand-off through a ring of SP_RING slots guarded by counters
+constexpr int SP_SPIN_CAP = 1 << 22; // a wave never spins longer than this (a bug shows as wrong bits, not a hang)
+
+__device__ __forceinline__ int sp_spin_until(__attribute__((address_space(3))) int *p, int target) {
+    int v = __builtin_amdgcn_readfirstlane(__atomic_load_n(p, __ATOMIC_RELAXED));
+    for (int g = 0; v < target && g < SP_SPIN_CAP; ++g) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __builtin_amdgcn_readfirstlane(__atomic_load_n(p, __ATOMIC_RELAXED));
+    }
+    return v;
+}
 
 // The workgroup barrier of one iteration.  Only LDS is ordered: the hand-off row
 // written before it is read after it.  Wave 0's row prefetch and the last wave's
@@ -94,7 +111,7 @@ __device__ __forceinline__ void sp_sync() {
 // stages [Q0, min(Q1, ACT)) on one row each, then the hand-off and the barrier.
 template <int K, int PD, int C, int NW, int S, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U>
 __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, S == 0> &St, const PsArgs &A,
-                                        const PsLane &L, const SpXfer &X, int i) {
+                                        const PsLane &L, SpXfer &X, int i) {
     using St_ = Stages<K, NW, S>;
     constexpr int Q0 = St_::Q0, Q1 = St_::Q1;
     constexpr int NR = PD + 2;
@@ -109,11 +126,27 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
             r0c[j] = St.ring[(U + NR - 1) % NR][j];
             r0f[j] = St.ring[U][j];
         }
+    } else if constexpr ((CP & SP_FLAGS) != 0) {
+        // stage Q0 - 1's output of local iteration T, slot T % NR (= U): wait until
+        // the producer has written it, read it, and free the slot
+        const int T = i - X.is;
+        if (X.seen_in <= T) X.seen_in = sp_spin_until(X.cnt_in, T + 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        double(&fr)[C] = P == 0 ? St.Wb[0] : St.Wa[0];
+        xfer_read<C>(fr, X.in + U * 64 * C, X.lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (X.lane == 0) __atomic_store_n(X.cnt_in + 1, T + 1, __ATOMIC_RELAXED);
     } else {
         // stage Q0 - 1's output of this local iteration, handed over one barrier
         // step ago (local iteration i of wave S-1 ran at step i + S - 1)
         double(&fr)[C] = P == 0 ? St.Wb[0] : St.Wa[0];
         xfer_read<C>(fr, X.in + ((U + S + 1) & 1) * 64 * C, X.lane);
+    }
+    if constexpr ((CP & SP_FLAGS) != 0 && S < NW - 1) {
+        // slot T % NR must have been read: the consumer has consumed row T - NR
+        const int T = i - X.is;
+        if (X.seen_out < T - NR + 1) X.seen_out = sp_spin_until(X.cnt_out + 1, T - NR + 1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
 #pragma unroll
     for (int q = Q0; q < (Q1 < ACT ? Q1 : ACT); ++q) {
@@ -131,7 +164,10 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
 #pragma unroll
             for (int j = 0; j < C; ++j) nx[j] = v[j];
         } else if (q + 1 < K) {
-            xfer_write<C>(X.out + ((U + S) & 1) * 64 * C, v, X.lane);
+            if constexpr ((CP & SP_FLAGS) != 0)
+                xfer_write<C>(X.out + U * 64 * C, v, X.lane);     // slot freed below, before the stages
+            else
+                xfer_write<C>(X.out + ((U + S) & 1) * 64 * C, v, X.lane);
         } else if (STORE) {
             if (SC) {
 #pragma unroll
@@ -140,12 +176,21 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
             vk_ps::ps_store<C, GL && GR && EY, CP & 2>(A.d + (int64_t)(i - K) * L.ny64, v, L);
         }
     }
-    sp_sync();
+    if constexpr ((CP & SP_FLAGS) != 0) {
+        if constexpr (S < NW - 1) {
+            // publish row T (written above, or not at all while stage Q1-1 has not
+            // joined the fill: the consumer's stage has not joined either)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (X.lane == 0) __atomic_store_n(X.cnt_out, i - X.is + 1, __ATOMIC_RELAXED);
+        }
+    } else {
+        sp_sync();
+    }
 }
 
 template <int K, int PD, int C, int NW, int S, bool GL, bool GR, bool EY, bool SC, int CP, int T>
 __device__ __forceinline__ void sp_fill(SpState<K, PD, C, Stages<K, NW, S>::NS, S == 0> &St, const PsArgs &A,
-                                        const PsLane &L, const SpXfer &X, int is) {
+                                        const PsLane &L, SpXfer &X, int is) {
     if constexpr (T < 2 * K - 1) {
         constexpr int ACT = T / 2 + 1 < K ? T / 2 + 1 : K;
         sp_iter<K, PD, C, NW, S, GL, GR, EY, SC, CP, ACT, false, T % (PD + 2)>(St, A, L, X, is + T);
@@ -155,7 +200,7 @@ __device__ __forceinline__ void sp_fill(SpState<K, PD, C, Stages<K, NW, S>::NS, 
 
 template <int K, int PD, int C, int NW, int S, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u>
 __device__ __forceinline__ void sp_tail(SpState<K, PD, C, Stages<K, NW, S>::NS, S == 0> &St, const PsArgs &A,
-                                        const PsLane &L, const SpXfer &X, int i, int n) {
+                                        const PsLane &L, SpXfer &X, int i, int n) {
     constexpr int NR = PD + 2;
     if constexpr (u < NR - 1) {
         if (u < n) {
@@ -168,7 +213,7 @@ __device__ __forceinline__ void sp_tail(SpState<K, PD, C, Stages<K, NW, S>::NS, 
 template <int K, int PD, int C, int NW, int S, bool GL, bool GR, bool EY, bool SC, int CP, int... Us>
 __device__ __forceinline__ void sp_steady(std::integer_sequence<int, Us...>,
                                           SpState<K, PD, C, Stages<K, NW, S>::NS, S == 0> &St, const PsArgs &A,
-                                          const PsLane &L, const SpXfer &X, int i, int i1) {
+                                          const PsLane &L, SpXfer &X, int i, int i1) {
     constexpr int NR = PD + 2;
     constexpr int PH = (2 * K - 1) % NR;
     for (; i + NR <= i1; i += NR) (sp_iter<K, PD, C, NW, S, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR>(St, A, L, X, i + Us), ...);
@@ -179,7 +224,7 @@ __device__ __forceinline__ void sp_steady(std::integer_sequence<int, Us...>,
 // the single-wave pipeline on its stages, NW-1-S idle steps -- every wave meets
 // the same 2K-1 + (c1-c0) + NW-1 barriers.
 template <int K, int PD, int C, int NW, int S, bool GL, bool GR, bool EY, bool SC, int CP>
-__device__ __forceinline__ void sp_body(const PsArgs &A, const PsLane &L, const SpXfer &X, int c0, int c1) {
+__device__ __forceinline__ void sp_body(const PsArgs &A, const PsLane &L, SpXfer &X, int c0, int c1) {
     constexpr int NR = PD + 2;
     using St_ = Stages<K, NW, S>;
     SpState<K, PD, C, St_::NS, S == 0> St;
@@ -194,14 +239,17 @@ __device__ __forceinline__ void sp_body(const PsArgs &A, const PsLane &L, const 
         for (int u = 0; u < PD; ++u)
             vk_ps::ps_load<C, GL && GR && EY, CP & 1>(St.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
     }
-    for (int b = 0; b < S; ++b) sp_sync();
+    X.is = is;
+    if constexpr ((CP & SP_FLAGS) == 0)
+        for (int b = 0; b < S; ++b) sp_sync();
     sp_fill<K, PD, C, NW, S, GL, GR, EY, SC, CP, 0>(St, A, L, X, is);
     sp_steady<K, PD, C, NW, S, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), St, A, L, X, c0 + K, c1 + K);
-    for (int b = S + 1; b < NW; ++b) sp_sync();
+    if constexpr ((CP & SP_FLAGS) == 0)
+        for (int b = S + 1; b < NW; ++b) sp_sync();
 }
 
 template <int K, int PD, int C, int NW, bool SC, int CP, int S = 0>
-__device__ __forceinline__ void sp_dispatch(int w, bool general, const PsArgs &A, const PsLane &L, const SpXfer &X,
+__device__ __forceinline__ void sp_dispatch(int w, bool general, const PsArgs &A, const PsLane &L, SpXfer &X,
                                             int c0, int c1) {
     if constexpr (S < NW) {
         if (w == S) {
@@ -225,10 +273,16 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
                                                        const double *__restrict__ uniform) {
     constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
-    __shared__ __attribute__((aligned(16))) double xfer[(NW > 1 ? NW - 1 : 1) * 2 * 64 * C];
+    constexpr int SLOTS = (CP & SP_FLAGS) ? PD + 2 : 2;     // hand-off slots per boundary
+    __shared__ __attribute__((aligned(16))) double xfer[(NW > 1 ? NW - 1 : 1) * SLOTS * 64 * C];
+    __shared__ int xcnt[2 * (NW > 1 ? NW - 1 : 1)];
     const int wg = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
+    if constexpr ((CP & SP_FLAGS) != 0) {
+        if (threadIdx.x < 2 * (NW - 1)) xcnt[threadIdx.x] = 0;
+        __syncthreads();
+    }
     const int tx = wg % tiles_x;
     const int ty = (wg / tiles_x) % chunks_y;
     const int f = wg / (tiles_x * chunks_y);
@@ -262,9 +316,14 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
     A.cK = cK;
     SpXfer X;
     lds_double *xl = (lds_double *)xfer;
-    X.in = xl + (w > 0 ? w - 1 : 0) * 2 * 64 * C;
-    X.out = xl + (w < NW - 1 ? w : 0) * 2 * 64 * C;
+    X.in = xl + (w > 0 ? w - 1 : 0) * SLOTS * 64 * C;
+    X.out = xl + (w < NW - 1 ? w : 0) * SLOTS * 64 * C;
     X.lane = lane;
+    __attribute__((address_space(3))) int *cl = (__attribute__((address_space(3))) int *)xcnt;
+    X.cnt_in = cl + 2 * (w > 0 ? w - 1 : 0);
+    X.cnt_out = cl + 2 * (w < NW - 1 ? w : 0);
+    X.seen_in = X.seen_out = 0;
+    X.is = 0;
     const bool gl = x0 - KH <= 0;
     const bool gr = x0 - KH + 64 * C >= ny;
     const bool ey = (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
@@ -293,3 +352,14 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
 }
 
 }  // namespace vk_sp
+
+// One split-pass variant as a launcher of its own (each vk_stencil_sp*.hip unit
+// instantiates two, so that they compile side by side); vk_launch_sp dispatches.
+#define VK_SP_DEFINE(VARIANT, K, PD, C, NW, CP)                                                                    \
+    void vk_sp_launch_##VARIANT(VK_STENCIL_LAUNCH_ARGS, int rows) {                                               \
+        (void)k;                                                                                                   \
+        (void)f0;                                                                                                  \
+        (void)cp;                                                                                                  \
+        vk_sp::launch<K, PD, C, NW, CP>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, \
+                                        rows);                                                                     \
+    }

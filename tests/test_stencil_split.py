@@ -19,7 +19,7 @@ from oracle import cpu
 torch = pytest.importorskip('torch')
 
 pytestmark = pytest.mark.gpu
-SPLIT = (40, 41, 42, 43, 44, 45, 46, 47)
+SPLIT = (40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51)
 
 
 @pytest.fixture(scope='module')
