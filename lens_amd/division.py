@@ -13,7 +13,13 @@ Restates what a dividing compartment needs from the reference:
   generated processes and topology, ids from ``daughter_phylogeny_id``;
 * ``GrowthProtein`` (vivarium/processes/growth_protein.py:20-107), the
   ``growth_division_minimal`` growth process (units removed: masses in fg,
-  protein as a count).
+  protein as a count), and the two derivers it asks for (``derivers()``):
+  ``TreeMass`` (tree_mass.py:10-65) and ``DeriveGlobals``
+  (derive_globals.py:17-150), with the scalars pint produces in the reference
+  evaluated as :class:`lens_amd.cells.CellModel` does for the device colony;
+* :func:`growth_division_minimal`, the compartment
+  (vivarium/compartments/growth_division_minimal.py:22-60 plus
+  process.py:75-103's generated derivers, which come first).
 
 The store side (``_divide`` / ``_generate`` / ``_delete`` / ``_add`` in
 ``Store.apply_update``, experiment.py:628-697) lives in
@@ -39,8 +45,8 @@ def divide_set(state):
 
 
 def divide_split(state):
-    """registry.py:205-236."""
-    if isinstance(state, (int, np.integer)) and not isinstance(state, bool):
+    """registry.py:205-236 (a bool is an int there too)."""
+    if isinstance(state, (int, np.integer)):
         remainder = state % 2
         half = int(state / 2)
         if random.choice([True, False]):
@@ -159,3 +165,107 @@ class GrowthProtein(ProcessBase):
             new_protein += 1
         return {'internal': {'protein': new_protein}, 'global': {'divide': bool(protein >= self.divide_protein)}}
 
+
+
+class TreeMass(ProcessBase):
+    """tree_mass.py:21-65: the agent's mass = initial_mass + the mass of every
+    count whose schema carries a molecular weight (``_properties.mw``), summed
+    over the agent's tree in store order (the ``_reduce`` update with
+    calculate_mass).  Here the counts with a weight are named by ``mw_paths``
+    ({path below the agent: g/mol}); the fg sum is CellModel.tree_mass's."""
+
+    name = 'mass_deriver'
+    defaults = {'initial_mass': 0.0, 'mw_paths': {}}
+
+    def __init__(self, initial_parameters=None):
+        super().__init__(initial_parameters)
+        self.mw_paths = dict(self.parameters['mw_paths'])
+
+    def is_deriver(self):
+        return True
+
+    def ports_schema(self):
+        init = self.parameters['initial_mass']
+        return {'global': {'initial_mass': {'_default': init, '_updater': 'set', '_divider': 'split'},
+                           'mass': {'_default': init, '_emit': True, '_updater': 'set', '_divider': 'split'}},
+                'agent': {}}
+
+    def next_update(self, timestep, states):
+        from lens_amd.cells import FG_PER_G
+        value = states['global']['initial_mass']
+        agent = states['agent']
+        for path, mw in self.mw_paths.items():
+            node = agent
+            for k in path:
+                node = node.get(k) if isinstance(node, dict) else None
+            if node is not None:
+                # calculate_mass: value + mw * (count / N_A), the g converted to fg
+                value = value + (mw * (node / AVOGADRO)) * FG_PER_G
+        return {'global': {'mass': value}}
+
+
+class DeriveGlobals(ProcessBase):
+    """derive_globals.py:54-150: volume, mmol_to_counts, length, surface area and
+    periplasm volume from the mass (capsule of the given width), in the
+    reference's operation order (CellModel.derive)."""
+
+    name = 'globals_deriver'
+    defaults = {'width': 1, 'initial_mass': 1339.0, 'periplasm_volume_fraction': 0.3, 'density': 1100.0}
+
+    def __init__(self, initial_parameters=None):
+        super().__init__(initial_parameters)
+        from lens_amd.cells import CellModel
+        p = self.parameters
+        self.model = CellModel(width=p['width'], density=p['density'], avogadro=AVOGADRO)
+
+    def is_deriver(self):
+        return True
+
+    def _derived(self, mass):
+        volume, m2c, length, area = self.model.derive(mass)
+        return {'volume': volume, 'mmol_to_counts': m2c, 'length': length, 'surface_area': area,
+                'periplasm_volume': volume * self.parameters['periplasm_volume_fraction']}
+
+    def ports_schema(self):
+        mass = self.parameters['initial_mass']
+        d = self._derived(mass)
+        default = {'mass': mass, 'volume': d['volume'], 'mmol_to_counts': d['mmol_to_counts'],
+                   'density': self.parameters['density'], 'width': self.parameters['width'],
+                   'length': d['length'], 'surface_area': d['surface_area'],
+                   'periplasm_volume': d['periplasm_volume']}
+        set_states = ('volume', 'mmol_to_counts', 'length', 'surface_area', 'periplasm_volume')
+        split = ('volume', 'length', 'surface_area', 'periplasm_volume')
+        emit = ('volume', 'width', 'length', 'surface_area')
+        schema = {}
+        for k, v in default.items():
+            s = {'_default': v}
+            if k in set_states:
+                s['_updater'] = 'set'
+            if k in emit:
+                s['_emit'] = True
+            if k in split:
+                s['_divider'] = 'split'
+            schema[k] = s
+        return {'global': schema}
+
+    def next_update(self, timestep, states):
+        return {'global': self._derived(states['global']['mass'])}
+
+
+def growth_division_minimal(agent_id, growth_rate=0.000275, boundary_path=('boundary',)):
+    """The growth_division_minimal compartment of one agent: processes and
+    topology, derivers first (process.py:179-182 merges them in front)."""
+    growth = GrowthProtein({'growth_rate': growth_rate})
+    return {
+        'processes': {
+            'mass_deriver': TreeMass({'mw_paths': {('internal', 'protein'): growth.parameters['protein_mw']}}),
+            'global_deriver': DeriveGlobals(),
+            'growth': growth,
+            'division': MetaDivision({'agent_id': agent_id, 'daughter_path': (),
+                                      'compartment': lambda cfg: growth_division_minimal(
+                                          cfg['agent_id'], growth_rate, boundary_path)})},
+        'topology': {
+            'mass_deriver': {'global': boundary_path, 'agent': ()},
+            'global_deriver': {'global': boundary_path},
+            'growth': {'internal': ('internal',), 'global': boundary_path},
+            'division': {'global': boundary_path, 'cells': ('..', '..', 'agents')}}}

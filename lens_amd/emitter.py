@@ -93,6 +93,29 @@ class ColonyEmitter:
         return path_timeseries_from_data(self.saved_data)
 
 
+class ExperimentEmitter:
+    """The in-memory timeseries emitter of the Process-API loop
+    (:class:`lens_amd.engine.Experiment`): ``emit()`` records
+    ``{time: experiment.emit_data() + extra}`` (Experiment.emit_data,
+    vivarium/core/experiment.py:1328-1336; TimeSeriesEmitter, emitter.py:150-164)."""
+
+    def __init__(self, experiment, extra=None):
+        self.experiment = experiment
+        self.extra = extra or {}
+        self.saved_data: Dict[float, dict] = {}
+
+    def emit(self, time: Optional[float] = None):
+        data = self.experiment.emit_data()
+        data.update(self.extra)
+        self.saved_data[self.experiment.local_time if time is None else time] = data
+
+    def get_data(self):
+        return self.saved_data
+
+    def get_path_timeseries(self):
+        return path_timeseries_from_data(self.saved_data)
+
+
 # ---------------------------------------------------------------------------
 # the reference's raw-data -> timeseries -> CSV transforms (restated)
 # ---------------------------------------------------------------------------

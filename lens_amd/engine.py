@@ -172,6 +172,7 @@ class Experiment:
         self._plans: Dict[Tuple, Tuple] = {}        # process path -> (version, process, kinetics plan)
         self._state_nodes: Dict[Tuple, Tuple] = {}  # process path -> (version, process, [(port, parent, key)])
         self._version = 0
+        self._emit_paths: Dict[Tuple, bool] = {}    # store paths with _emit (ordered set)
         self._proc_index = _PathIndex()            # process paths with cached port entries (tag: port)
         self._schema_index = _PathIndex()          # store paths with a schema updater / divider
         self.dividers: Dict[Tuple, object] = {}   # store path (with '*' globs) -> schema _divider
@@ -237,9 +238,12 @@ class Experiment:
         self._version += 1
         self._clear_leaf_caches()
         keys = [k for k in schema if not k.startswith('_')]
-        if ('_default' in schema or '_value' in schema or '_updater' in schema or '_divider' in schema) and not keys:
-            if '_updater' in schema or '_divider' in schema:
+        if ('_default' in schema or '_value' in schema or '_updater' in schema or '_divider' in schema or
+                '_emit' in schema) and not keys:
+            if '_updater' in schema or '_divider' in schema or schema.get('_emit'):
                 self._schema_index.add(path)
+            if schema.get('_emit'):
+                self._emit_paths[path] = True       # Store.emit (experiment.py:299), in registration order
             if '_updater' in schema:           # a schema without one keeps the store's updater
                 self.schema.setdefault(path, schema['_updater'])
                 if '*' in path and path not in self._globs:
@@ -483,6 +487,7 @@ class Experiment:
         for spath, _ in self._schema_index.pop_prefix(path):
             self.schema.pop(spath, None)
             self.dividers.pop(spath, None)
+            self._emit_paths.pop(spath, None)
             if spath in self._globs:
                 self._globs.remove(spath)
             if spath in self._div_globs:
@@ -728,6 +733,35 @@ class Experiment:
             if id(deriver) in self._deleted:          # removed by an earlier deriver's _divide / _delete
                 continue
             self.apply_update(deriver.next_update(0, self.process_states(path, deriver)), path)
+
+    def emit_data(self):
+        """Store.emit_data (experiment.py:463-481): the values of the stores whose
+        schema sets ``_emit``, as a nested dict (branches in the order their first
+        emitted leaf was registered; a '*' in a path matches every child, in store
+        order).  Stores that are gone are skipped."""
+        out = {}
+
+        def put(path, value):
+            node = out
+            for k in path[:-1]:
+                node = node.setdefault(k, {})
+            node[path[-1]] = value
+
+        def expand(node, path, rest):
+            if not rest:
+                put(path, node)
+                return
+            if not isinstance(node, dict):
+                return
+            k = rest[0]
+            if k == '*':
+                for child, sub in node.items():
+                    expand(sub, path + (child,), rest[1:])
+            elif k in node:
+                expand(node[k], path + (k,), rest[1:])
+        for path in self._emit_paths:
+            expand(self.state, (), path)
+        return out
 
     # -- Experiment.update (experiment.py:1351-1450) ---------------------------------
     def update(self, interval):
