@@ -160,6 +160,22 @@ int vk_step_dopri5(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
                    double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
                    vk_stream_t stream);
 
+/* vk_step_dopri5 (variant 2, after vk_table_specialize) fused with the
+ * gather of the NEXT step's local environment: once agent a is integrated,
+ * conc[map_row[i] * ld + a] = fields[map_field[i] * field_stride + bin_lin[a]]
+ * for i < n_map (<= 8) -- the values vk_gather writes when it runs right after
+ * the kinetics (DiffusionField.get_local_environments, diffusion_field.py:
+ * 362-379, feeding ConvenienceKinetics.next_update, convenience_kinetics.py:
+ * 303-352, one step later).  One launch and one sweep of the field lines
+ * instead of two.                                                          */
+int vk_step_dopri5_gather(const vk_table *t, int64_t n_agents, int64_t ld, double dt,
+                          const vk_ode_opts *opts, const double *params, double *conc,
+                          const double *mmol_to_counts, double *h_state, double *flux,
+                          int64_t *counts, int32_t *status, int32_t *nsteps,
+                          const double *fields, int64_t field_stride, const int32_t *bin_lin,
+                          const int32_t *map_field, const int32_t *map_row, int32_t n_map,
+                          vk_stream_t stream);
+
 /* n_steps consecutive agent-steps of dt in one launch, for colonies whose
  * agents do not couple between steps (held externals; BASELINE config 2):
  * every step is vk_step_dopri5 variant 2's, bit for bit, with the state kept

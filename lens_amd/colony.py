@@ -74,6 +74,10 @@ class Colony:
         # by default: on one MI355X at C4 the coupled step ran 1.533 ms against 1.511
         # with the separate launches (profiles/r04/r04h/couple_ab.log)
         self.fuse_coupling = False
+        # lattice colonies on the specialised agent-per-lane DP45 kernel: the gather of
+        # the next step's local environment rides on the kinetics launch
+        # (vk_step_dopri5_gather; the same values as vk_gather right after it)
+        self.fuse_gather = True
         self._couple = None
         self.last_step_coupled = False
         self._comm_stream = torch.cuda.Stream(self.device) if self.device.type == 'cuda' else None
@@ -275,6 +279,24 @@ class Colony:
         self._layout += 1            # captured graphs hold the old occupancy buffers
         return self.agent_order
 
+    def _gather_fused(self):
+        """Whether this step's kinetics launch also does the gather."""
+        return (self.fuse_gather and self.lattice is not None and self.integrator == 'dopri5' and
+                self.engine.default_variant() == 2 and 0 < self.map_gather_field.numel() <= 8)
+
+    def kinetics_and_gather(self, dt: float):
+        """kinetics(dt) then gather_external(), as one launch when the kernel allows."""
+        if not self._gather_fused():
+            self.kinetics(dt)
+            self.gather_external()
+            return
+        lat = self.lattice
+        self.engine.dopri5_gather(dt, self.params, self.conc, self.m2c, self.n, self.h_state, self.rtol, self.atol,
+                                  self.max_steps, self.flux, self.counts, self.status, self.nsteps, lat.fields,
+                                  lat.field_stride, self.bin_lin, self.map_gather_field, self.map_gather_row)
+        if getattr(self, 'attempts', None) is not None:
+            self.attempts += self.nsteps[:self.n].sum()
+
     def gather_external(self):
         """external := field at the agent's bin (get_local_environments)."""
         self.lattice.gather(self.bin_lin, self.n, self.map_gather_field, self.map_gather_row, self.conc)
@@ -372,7 +394,14 @@ class Colony:
             halo_done = self.lattice.exchange_first_halo(dt, halo_exchange, self._comm_stream)
         if 'kin' in timing:
             timing['kin'][0].record()
-        self.kinetics(dt)
+        coupled = (self.lattice is not None and halo_done is None and halo_exchange is None and
+                   self.fuse_coupling and self._couple is not None and self.exchange_mode == 'sorted' and
+                   self.lattice.coupled_plan_ok(dt))
+        fused = self.lattice is not None and not coupled and self._gather_fused()
+        if fused:
+            self.kinetics_and_gather(dt)                     # + the pre-step field (one-step lag)
+        else:
+            self.kinetics(dt)
         if 'kin' in timing:
             timing['kin'][1].record()
         if stamp is not None:
@@ -380,7 +409,8 @@ class Colony:
         if self.lattice is not None:
             lat = self.lattice
             if not (halo_done is None and halo_exchange is None and self._coupled_step(dt, allreduce, timing)):
-                self.gather_external()                       # pre-step field (one-step lag)
+                if not fused:
+                    self.gather_external()                   # pre-step field (one-step lag)
                 if halo_done is not None:
                     torch.cuda.current_stream(self.device).wait_event(halo_done)
                 lat.diffuse(dt, halo_exchange=halo_exchange, allreduce=allreduce,

@@ -32,6 +32,7 @@ struct vk_table {
     hipFunction_t spec_dopri5 = nullptr;      // agent per lane (variant 2)
     hipFunction_t spec_wave = nullptr;        // agent per wavefront (variant 3)
     hipFunction_t spec_multi = nullptr;       // agent per lane, several steps per launch (vk_step_dopri5_multi)
+    hipFunction_t spec_gather = nullptr;      // agent per lane + the next step's gather (vk_step_dopri5_gather)
 };
 
 // Load through the constant address space: uniform index -> s_load (scalar cache).

@@ -208,8 +208,9 @@ extern "C" int vk_table_specialize(vk_table *t, const char *source) {
     int rc = vk::hip_check(hipModuleLoadData(&mod, code.data()), "hipModuleLoadData(spec)");
     if (rc) return rc;
     // the source defines the agent-per-lane kernel, the agent-per-wavefront one, or both
-    hipFunction_t fn = nullptr, fw = nullptr, fm = nullptr;
+    hipFunction_t fn = nullptr, fw = nullptr, fm = nullptr, fg = nullptr;
     if (hipModuleGetFunction(&fn, mod, "vk_dopri5_spec") != hipSuccess) fn = nullptr;
+    if (hipModuleGetFunction(&fg, mod, "vk_dopri5_spec_gather") != hipSuccess) fg = nullptr;
     if (hipModuleGetFunction(&fw, mod, "vk_dopri5_wspec") != hipSuccess) fw = nullptr;
     if (hipModuleGetFunction(&fm, mod, "vk_dopri5_spec_multi") != hipSuccess) fm = nullptr;
     (void)hipGetLastError();
@@ -223,6 +224,7 @@ extern "C" int vk_table_specialize(vk_table *t, const char *source) {
     t->spec_dopri5 = fn;
     t->spec_wave = fw;
     t->spec_multi = fm;
+    t->spec_gather = fg;
     return VK_OK;
 }
 
@@ -997,6 +999,41 @@ static int launch_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, co
 }
 
 // n_steps agent-steps of dt per launch for agents that do not couple between
+// One vk_step_dopri5 (variant 2) that also gathers the next step's local
+// environment: after the integration, conc[map_row[i] * ld + a] := plane
+// map_field[i] of `fields` at bin_lin[a], as vk_gather right after the kinetics.
+extern "C" int vk_step_dopri5_gather(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,
+                                     const double *params, double *conc, const double *m2c, double *h_state,
+                                     double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
+                                     const double *fields, int64_t field_stride, const int32_t *bin_lin,
+                                     const int32_t *map_field, const int32_t *map_row, int32_t n_map,
+                                     vk_stream_t stream) {
+    int rc = check_agents("vk_step_dopri5_gather", t, n, ld);
+    if (rc || n == 0) return rc;
+    if (!o || !params || !conc || !m2c || !flux || (!counts && t->dev.n_ext > 0) || n_map < 0 || n_map > 8 ||
+        (n_map > 0 && (!fields || !bin_lin || !map_field || !map_row))) {
+        vk::set_error("vk_step_dopri5_gather: null argument or n_map outside [0, 8]");
+        return VK_ERR_ARG;
+    }
+    if (!(dt > 0.0) || !(o->rtol > 0.0) || !(o->atol >= 0.0) || o->max_steps <= 0) {
+        vk::set_error("vk_step_dopri5_gather: need dt > 0, rtol > 0, atol >= 0, max_steps > 0");
+        return VK_ERR_ARG;
+    }
+    if (!t->spec_gather) {
+        vk::set_error("vk_step_dopri5_gather: needs vk_table_specialize with an agent-per-lane source first");
+        return VK_ERR_ARG;
+    }
+    double rtol = o->rtol, atol = o->atol;
+    int max_steps = o->max_steps, nm = n_map;
+    void *args[] = {&n, &ld, &dt, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c, &h_state,
+                    &flux, &counts, &status, &nsteps, (void *)&fields, &field_stride, (void *)&bin_lin,
+                    (void *)&map_field, (void *)&map_row, &nm};
+    const unsigned blocks = (unsigned)((n + 255) / 256);
+    return vk::hip_check(hipModuleLaunchKernel(t->spec_gather, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream,
+                                               args, nullptr),
+                         "hipModuleLaunchKernel(vk_dopri5_spec_gather)");
+}
+
 // steps (held externals), with the network-specialised agent-per-lane kernel.
 extern "C" int vk_step_dopri5_multi(const vk_table *t, int64_t n, int64_t ld, double dt, int32_t n_steps,
                                     const vk_ode_opts *o, const double *params, double *conc, const double *m2c,

@@ -210,6 +210,33 @@ class KineticsEngine:
             native.stream_handle()), 'vk_step_dopri5_multi')
         return flux, counts, status, nsteps
 
+    def dopri5_gather(self, dt, params, conc, mmol_to_counts, n_agents, h_state, rtol, atol, max_steps, flux,
+                      counts, status, nsteps, fields, field_stride, bin_lin, map_field, map_row):
+        """One :meth:`dopri5` step (variant 2) that also writes the next step's
+        local environment: conc[map_row[i], a] := plane map_field[i] of ``fields``
+        at bin_lin[a] (vk_step_dopri5_gather) -- what a vk_gather right after the
+        kinetics writes."""
+        if self.default_variant() != 2:
+            raise native.NativeError('dopri5_gather needs the specialised agent-per-lane kernel (specialize())')
+        n = int(n_agents)
+        ld = self._check_state(params, conc, n)
+        for name, x in (('mmol_to_counts', mmol_to_counts), ('h_state', h_state)):
+            _need(x, name, None, ld, F64, self.device)
+        _need(flux, 'flux', self.table.n_reactions, ld, F64, self.device)
+        _need(counts, 'counts', self.table.n_ext, ld, torch.int64, self.device)
+        _need(status, 'status', None, ld, torch.int32, self.device)
+        _need(nsteps, 'nsteps', None, ld, torch.int32, self.device)
+        n_map = int(map_field.numel())
+        if n_map != int(map_row.numel()) or n_map > 8:
+            raise ValueError('dopri5_gather: map_field / map_row of equal length <= 8')
+        opts = native.VkOdeOpts(float(rtol), float(atol), int(max_steps), 2)
+        native.check(native._lib.vk_step_dopri5_gather(
+            self.dev.handle, n, ld, float(dt), ctypes.byref(opts), native.ptr(params), native.ptr(conc),
+            native.ptr(mmol_to_counts), native.ptr(h_state), native.ptr(flux), native.ptr(counts),
+            native.ptr(status), native.ptr(nsteps), native.ptr(fields), int(field_stride), native.ptr(bin_lin),
+            native.ptr(map_field), native.ptr(map_row), n_map, native.stream_handle()), 'vk_step_dopri5_gather')
+        return flux, counts, status, nsteps
+
     def dopri5_flops_per_attempt(self) -> int:
         """6 RHS evaluations + stage combinations + error norm per attempted step."""
         ny = self.table.n_dyn + self.table.n_reactions

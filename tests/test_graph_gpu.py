@@ -206,3 +206,29 @@ def test_overlapped_capture_equals_sequential_steps(dev, steps):
         for name in ('conc', 'flux', 'counts', 'h_state', 'nsteps'):
             assert torch.equal(getattr(c, name)[..., :c.n], getattr(ref, name)[..., :ref.n]), name
         assert torch.equal(c.lattice.fields, ref.lattice.fields)
+
+
+@pytest.mark.parametrize('sort', [False, True])
+def test_fused_gather_equals_separate_gather(dev, sort):
+    """vk_step_dopri5_gather (the kinetics launch gathering the next step's local
+    environment) against vk_step_dopri5 + vk_gather: every agent array and both
+    fields bit for bit after several lattice steps, eager and graph-replayed,
+    with agents in generated and in bin order."""
+    a, b, c = _lattice_colony(dev), _lattice_colony(dev), _lattice_colony(dev)
+    a.fuse_gather = False
+    assert b._gather_fused() and not a._gather_fused()
+    for col in (a, b, c):
+        if sort:
+            col.sort_by_bin()
+    for _ in range(4):
+        a.step(1.0)
+        b.step(1.0)
+    replay = c.capture(1.0, 4)
+    replay()
+    torch.cuda.synchronize()
+    n = a.n
+    for col in (b, c):
+        for name in ('conc', 'h_state', 'flux', 'counts', 'nsteps', 'status'):
+            x, y = getattr(a, name), getattr(col, name)
+            assert torch.equal(x[..., :n], y[..., :n]), name
+        assert torch.equal(col.lattice.fields, a.lattice.fields)
