@@ -135,6 +135,8 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
     the full template argument list, as rocprofv3 prints it.  ``pass_bytes``
     (source + destination rows of one pass): a 10-deep pass of at most 192 MiB
     stores through the caches (vk_stencil_ps10.hip), CP = 2."""
+    if mode == 'fma' and variant == 40 and depth == 10:
+        return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
     if mode == 'fma' and variant >= 20 and depth <= 11 and (depth % 2 == 1 or depth == 10):
         # k_diffuse_ps<K, PD, C, SC, CP> (vk_stencil_ps.h); SC = the rescaled form (coef not ~1/4)
         if variant == 30 and depth in (9, 10):
@@ -170,10 +172,12 @@ def parse(argv=None):
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=20, choices=[2, 3, 6, 20, 30],
-                   help='tolerance mode: 20 = pair-sum passes (default), 30 = pair-sum with the stage-0 ring '
-                        'held as 16-B vectors, 6 = the variant-6 FMA form; exact mode: 2 / 3 = wave tiles '
-                        'prefetching 3 / 6 rows, 6 (and 20, 30) = 3 with streaming stores')
+    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 30, 40],
+                   help='tolerance mode: 20 = pair-sum passes (default on one GPU), 30 = pair-sum with the '
+                        'stage-0 ring held as 16-B vectors, 40 = the 10-deep pair-sum pass with its stages split '
+                        'over a workgroup\'s waves (default on row bands), 6 = the variant-6 FMA form; exact '
+                        'mode: 2 / 3 = wave tiles prefetching 3 / 6 rows, 6 (and 20, 30, 40) = 3 with streaming '
+                        'stores')
     p.add_argument('--stencil-depth', type=int, default=None,
                    help='substeps fused per HBM pass (odd, or 10: tolerance-mode whole steps as 10-deep passes); '
                         'default 10 for C4 in the fma mode, else 9')
@@ -221,6 +225,13 @@ def stencil_settings(args, world):
         # (exact mode too since round 4: 1.830 / 1.850 / 1.827 against 1.873 / 1.867 / 1.908 ms
         # per C4 step at depth 9, profiles/r04/r04af/)
         depth = 10 if args.workload == 'c4' else 9
+    kernel = args.stencil_kernel
+    if kernel is None:
+        # row bands (N > 1) in the tolerance mode: the stage-split 10-deep pass, whose
+        # taller chunks fill a band's passes better (a middle rank's step at N = 8 / 4 /
+        # 2: 0.335 / 0.499 / 0.792 against 0.372 / 0.544 / 0.884 ms with variant 20,
+        # profiles/r05/r05fg/); the whole plane keeps variant 20
+        kernel = 40 if (world > 1 and args.stencil_mode == 'fma' and depth == 10) else 20
     rows = args.stencil_rows
     if rows is None:
         # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of
@@ -228,7 +239,7 @@ def stencil_settings(args, world):
         # substeps, profiles/r03/r03h_stencil_rows_sweep.log, r03k_sweep.log); else the
         # auto rule (chunk_rows)
         rows = 34 if (world == 1 and args.workload == 'c4') else 0
-    return args.stencil_mode, depth, args.stencil_kernel, rows
+    return args.stencil_mode, depth, kernel, rows
 
 
 def settle_steps_needed(warmup_s: float, warmup_steps: int, settle_ms: float, cap: int = 2000) -> int:

@@ -79,24 +79,7 @@ struct SpXfer {
     lds_double *in;      // boundary (S-1 -> S): slots of 64 * C doubles (unused by wave 0)
     lds_double *out;     // boundary (S -> S+1) (unused by the last wave)
     int lane;
-    // CP bit 3 (flag-synchronised ring, no barrier): per boundary two LDS counters,
-    // [0] rows written by the producer, [1] rows read by the consumer
-    __attribute__((address_space(3))) int *cnt_in, *cnt_out;
-    int seen_in, seen_out;   // last counter values this wave observed (wave-uniform)
-    int is;                  // the chunk's first local iteration (row index of T = 0)
 };
-
-constexpr int SP_FLAGS = 8;          // CP bit: hand-off through a ring of SP_RING slots guarded by counters
-constexpr int SP_SPIN_CAP = 1 << 22; // a wave never spins longer than this (a bug shows as wrong bits, not a hang)
-
-__device__ __forceinline__ int sp_spin_until(__attribute__((address_space(3))) int *p, int target) {
-    int v = __builtin_amdgcn_readfirstlane(__atomic_load_n(p, __ATOMIC_RELAXED));
-    for (int g = 0; v < target && g < SP_SPIN_CAP; ++g) {
-        __builtin_amdgcn_s_sleep(1);
-        v = __builtin_amdgcn_readfirstlane(__atomic_load_n(p, __ATOMIC_RELAXED));
-    }
-    return v;
-}
 
 // The workgroup barrier of one iteration.  Only LDS is ordered: the hand-off row
 // written before it is read after it.  Wave 0's row prefetch and the last wave's
@@ -126,27 +109,11 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
             r0c[j] = St.ring[(U + NR - 1) % NR][j];
             r0f[j] = St.ring[U][j];
         }
-    } else if constexpr ((CP & SP_FLAGS) != 0) {
-        // stage Q0 - 1's output of local iteration T, slot T % NR (= U): wait until
-        // the producer has written it, read it, and free the slot
-        const int T = i - X.is;
-        if (X.seen_in <= T) X.seen_in = sp_spin_until(X.cnt_in, T + 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-        double(&fr)[C] = P == 0 ? St.Wb[0] : St.Wa[0];
-        xfer_read<C>(fr, X.in + U * 64 * C, X.lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if (X.lane == 0) __atomic_store_n(X.cnt_in + 1, T + 1, __ATOMIC_RELAXED);
     } else {
         // stage Q0 - 1's output of this local iteration, handed over one barrier
         // step ago (local iteration i of wave S-1 ran at step i + S - 1)
         double(&fr)[C] = P == 0 ? St.Wb[0] : St.Wa[0];
         xfer_read<C>(fr, X.in + ((U + S + 1) & 1) * 64 * C, X.lane);
-    }
-    if constexpr ((CP & SP_FLAGS) != 0 && S < NW - 1) {
-        // slot T % NR must have been read: the consumer has consumed row T - NR
-        const int T = i - X.is;
-        if (X.seen_out < T - NR + 1) X.seen_out = sp_spin_until(X.cnt_out + 1, T - NR + 1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
 #pragma unroll
     for (int q = Q0; q < (Q1 < ACT ? Q1 : ACT); ++q) {
@@ -164,10 +131,7 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
 #pragma unroll
             for (int j = 0; j < C; ++j) nx[j] = v[j];
         } else if (q + 1 < K) {
-            if constexpr ((CP & SP_FLAGS) != 0)
-                xfer_write<C>(X.out + U * 64 * C, v, X.lane);     // slot freed below, before the stages
-            else
-                xfer_write<C>(X.out + ((U + S) & 1) * 64 * C, v, X.lane);
+            xfer_write<C>(X.out + ((U + S) & 1) * 64 * C, v, X.lane);
         } else if (STORE) {
             if (SC) {
 #pragma unroll
@@ -176,16 +140,7 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
             vk_ps::ps_store<C, GL && GR && EY, CP & 2>(A.d + (int64_t)(i - K) * L.ny64, v, L);
         }
     }
-    if constexpr ((CP & SP_FLAGS) != 0) {
-        if constexpr (S < NW - 1) {
-            // publish row T (written above, or not at all while stage Q1-1 has not
-            // joined the fill: the consumer's stage has not joined either)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-            if (X.lane == 0) __atomic_store_n(X.cnt_out, i - X.is + 1, __ATOMIC_RELAXED);
-        }
-    } else {
-        sp_sync();
-    }
+    sp_sync();
 }
 
 template <int K, int PD, int C, int NW, int S, bool GL, bool GR, bool EY, bool SC, int CP, int T>
@@ -239,13 +194,10 @@ __device__ __forceinline__ void sp_body(const PsArgs &A, const PsLane &L, SpXfer
         for (int u = 0; u < PD; ++u)
             vk_ps::ps_load<C, GL && GR && EY, CP & 1>(St.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
     }
-    X.is = is;
-    if constexpr ((CP & SP_FLAGS) == 0)
-        for (int b = 0; b < S; ++b) sp_sync();
+    for (int b = 0; b < S; ++b) sp_sync();
     sp_fill<K, PD, C, NW, S, GL, GR, EY, SC, CP, 0>(St, A, L, X, is);
     sp_steady<K, PD, C, NW, S, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), St, A, L, X, c0 + K, c1 + K);
-    if constexpr ((CP & SP_FLAGS) == 0)
-        for (int b = S + 1; b < NW; ++b) sp_sync();
+    for (int b = S + 1; b < NW; ++b) sp_sync();
 }
 
 template <int K, int PD, int C, int NW, bool SC, int CP, int S = 0>
@@ -273,16 +225,11 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
                                                        const double *__restrict__ uniform) {
     constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
-    constexpr int SLOTS = (CP & SP_FLAGS) ? PD + 2 : 2;     // hand-off slots per boundary
+    constexpr int SLOTS = 2;     // hand-off slots per boundary
     __shared__ __attribute__((aligned(16))) double xfer[(NW > 1 ? NW - 1 : 1) * SLOTS * 64 * C];
-    __shared__ int xcnt[2 * (NW > 1 ? NW - 1 : 1)];
     const int wg = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
-    if constexpr ((CP & SP_FLAGS) != 0) {
-        if (threadIdx.x < 2 * (NW - 1)) xcnt[threadIdx.x] = 0;
-        __syncthreads();
-    }
     const int tx = wg % tiles_x;
     const int ty = (wg / tiles_x) % chunks_y;
     const int f = wg / (tiles_x * chunks_y);
@@ -319,11 +266,6 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
     X.in = xl + (w > 0 ? w - 1 : 0) * SLOTS * 64 * C;
     X.out = xl + (w < NW - 1 ? w : 0) * SLOTS * 64 * C;
     X.lane = lane;
-    __attribute__((address_space(3))) int *cl = (__attribute__((address_space(3))) int *)xcnt;
-    X.cnt_in = cl + 2 * (w > 0 ? w - 1 : 0);
-    X.cnt_out = cl + 2 * (w < NW - 1 ? w : 0);
-    X.seen_in = X.seen_out = 0;
-    X.is = 0;
     const bool gl = x0 - KH <= 0;
     const bool gr = x0 - KH + 64 * C >= ny;
     const bool ey = (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
@@ -352,14 +294,3 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
 }
 
 }  // namespace vk_sp
-
-// One split-pass variant as a launcher of its own (each vk_stencil_sp*.hip unit
-// instantiates two, so that they compile side by side); vk_launch_sp dispatches.
-#define VK_SP_DEFINE(VARIANT, K, PD, C, NW, CP)                                                                    \
-    void vk_sp_launch_##VARIANT(VK_STENCIL_LAUNCH_ARGS, int rows) {                                               \
-        (void)k;                                                                                                   \
-        (void)f0;                                                                                                  \
-        (void)cp;                                                                                                  \
-        vk_sp::launch<K, PD, C, NW, CP>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, \
-                                        rows);                                                                     \
-    }

@@ -1,4 +1,4 @@
-"""Stage-split pair-sum passes (variants 40-43, vk_stencil_sp.h) against the
+"""Stage-split pair-sum passes (variant 40, vk_stencil_sp.h) against the
 single-wave pair-sum passes (variant 20, vk_stencil_ps.h).
 
 A split pass spreads the K stages of one tile over the waves of a workgroup
@@ -19,7 +19,7 @@ from oracle import cpu
 torch = pytest.importorskip('torch')
 
 pytestmark = pytest.mark.gpu
-SPLIT = (40, 41, 42, 43, 44, 45, 46, 47, 48, 49, 50, 51)
+SPLIT = (40,)
 
 
 @pytest.fixture(scope='module')
@@ -89,7 +89,7 @@ def test_split_pass_coefficient_forms(dev, variant, diffusion):
         assert np.array_equal(got.owned('a').cpu().numpy(), f0)
 
 
-@pytest.mark.parametrize('variant', [40, 42])
+@pytest.mark.parametrize('variant', SPLIT)
 def test_split_pass_vs_c_oracle(dev, variant):
     """Independent of variant 20: the C oracle's exact-order stencil, 1e-13."""
     rng = np.random.default_rng(11)
@@ -100,7 +100,7 @@ def test_split_pass_vs_c_oracle(dev, variant):
     assert float(np.abs(got - ref).max() / np.abs(ref).max()) < 1e-13
 
 
-@pytest.mark.parametrize('variant', [40, 42])
+@pytest.mark.parametrize('variant', SPLIT)
 def test_split_pass_row_bands_equal_whole_plane(dev, variant):
     """Row bands with one 100-deep halo block per step (the C4 bench at N > 1),
     stepped with the split passes, equal the whole plane bit for bit."""
