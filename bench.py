@@ -535,7 +535,10 @@ def main():
     if world > 1 and lat is not None:
         from lens_amd.distributed import make_halo_exchange, make_uniform_allreduce
         halo_ex = make_halo_exchange(lat, rank, world)
-        allred = make_uniform_allreduce()
+        # the uniform summary's all-reduce gets a communicator of its own: on the default
+        # group it would queue behind the first halo exchange (one NCCL stream per group)
+        # and the band's interior passes, which need the summary, could not overlap it
+        allred = make_uniform_allreduce(group=dist.new_group(list(range(world))))
     elif world > 1 and col.cells is not None:
         # agent-sharded C5: divisions are rank-local; even the shards out when
         # they drift more than 5 % apart (one all_to_all)

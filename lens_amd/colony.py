@@ -411,10 +411,10 @@ class Colony:
             if not (halo_done is None and halo_exchange is None and self._coupled_step(dt, allreduce, timing)):
                 if not fused:
                     self.gather_external()                   # pre-step field (one-step lag)
-                if halo_done is not None:
-                    torch.cuda.current_stream(self.device).wait_event(halo_done)
+                # with the first halo exchange in flight, the band's interior passes run
+                # first and the launch stream waits for the halo before the edge passes
                 lat.diffuse(dt, halo_exchange=halo_exchange, allreduce=allreduce,
-                            events=timing.get('diff'), halo_ready=halo_done is not None)
+                            events=timing.get('diff'), halo_event=halo_done)
                 self._step_exchange()
         elif self.environment == 'nonspatial':
             if self.map_exch_count.numel():
@@ -704,14 +704,25 @@ class Colony:
         t0, s0 = self.time, self.step_index
         g_kin = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_kin):
-            self.kinetics(dt)
-            self.gather_external()                       # pre-step field (one-step lag)
+            self.kinetics_and_gather(dt)                 # + the pre-step field (one-step lag)
             lat.uniform_summary(None)                    # the probe; its all-reduce is eager
+        # the first block's interior needs no halo: it is its own graph, replayed while
+        # the first halo exchange is in flight; the block's edges follow the halo
+        g_interior = None
+        if self.overlap_halo and self._comm_stream is not None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                j0, c0 = blocks[0]
+                split = lat._run_part(j0, c0, n_sub, coeff_dt, lat.uniform, lo_min, hi_max, native.VK_PART_INTERIOR)
+            g_interior = g if split else None
         g_blocks = []
         for b, (j, cnt) in enumerate(blocks):
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                lat._run_block(j, cnt, n_sub, coeff_dt, lat.uniform, lo_min, hi_max)
+                if b == 0 and g_interior is not None:
+                    lat._run_part(j, cnt, n_sub, coeff_dt, lat.uniform, lo_min, hi_max, native.VK_PART_EDGES)
+                else:
+                    lat._run_block(j, cnt, n_sub, coeff_dt, lat.uniform, lo_min, hi_max)
                 if b == len(blocks) - 1:
                     self._step_exchange()
             g_blocks.append(g)
@@ -728,6 +739,8 @@ class Colony:
             if allreduce is not None:
                 allreduce(lat.uniform)
             if halo_done is not None:
+                if g_interior is not None:
+                    g_interior.replay()                  # beside the halo exchange
                 main.wait_event(halo_done)
             else:
                 halo_exchange(lat.state_buffer(0), blocks[0][1])
@@ -739,6 +752,7 @@ class Colony:
             self.step_index += 1
 
         step.graphs = (g_kin, g_blocks)
+        step.interior_graph = g_interior
         return step
 
     def _finish_step(self, dt):

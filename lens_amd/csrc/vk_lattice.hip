@@ -209,11 +209,50 @@ static std::vector<int> odd_plan(int sub_count) {
     return ks;
 }
 
+static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
+                        int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max, int32_t edge_top,
+                        int32_t edge_bot, int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
+                        const double *uniform, int32_t part, vk_stream_t stream);
+
 extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                           int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
                           int32_t hi_max, int32_t edge_top, int32_t edge_bot, int32_t sub_begin,
                           int32_t sub_count, int32_t n_sub, double coeff_dt, const double *uniform,
                           vk_stream_t stream) {
+    return diffuse_impl(field, work0, work1, n_fields, field_stride, ny, row_lo, row_hi, lo_min, hi_max, edge_top,
+                        edge_bot, sub_begin, sub_count, n_sub, coeff_dt, uniform, VK_PART_ALL, stream);
+}
+
+// Whether vk_diffuse_part can split this block: the 10-deep plan of a row band's
+// block of 10 k substeps whose owned rows keep an interior through every pass.
+static bool part_plan_ok(int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max, int32_t sub_count,
+                         int32_t edge_top, int32_t edge_bot) {
+    const bool halo_top = !edge_top && row_lo > lo_min, halo_bot = !edge_bot && row_hi < hi_max;
+    return g_stencil_depth == 10 && sub_count % 10 == 0 && sub_count > 0 && (halo_top || halo_bot) &&
+           row_hi - row_lo > 2 * sub_count;
+}
+
+extern "C" int vk_diffuse_part(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
+                               int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max,
+                               int32_t edge_top, int32_t edge_bot, int32_t sub_begin, int32_t sub_count,
+                               int32_t n_sub, double coeff_dt, const double *uniform, int32_t part,
+                               vk_stream_t stream) {
+    if (part != VK_PART_ALL && part != VK_PART_INTERIOR && part != VK_PART_EDGES) {
+        vk::set_error("vk_diffuse_part: part must be VK_PART_ALL / _INTERIOR / _EDGES");
+        return VK_ERR_ARG;
+    }
+    if (part != VK_PART_ALL && !part_plan_ok(row_lo, row_hi, lo_min, hi_max, sub_count, edge_top, edge_bot)) {
+        vk::set_error("vk_diffuse_part: the block is not a 10-deep-plan band block with an interior");
+        return VK_ERR_LIMIT;
+    }
+    return diffuse_impl(field, work0, work1, n_fields, field_stride, ny, row_lo, row_hi, lo_min, hi_max, edge_top,
+                        edge_bot, sub_begin, sub_count, n_sub, coeff_dt, uniform, part, stream);
+}
+
+static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
+                        int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max, int32_t edge_top,
+                        int32_t edge_bot, int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
+                        const double *uniform, int32_t part, vk_stream_t stream) {
     if (!field || n_fields < 0 || ny <= 0 || row_lo < lo_min || row_hi > hi_max || row_lo >= row_hi ||
         sub_begin < 0 || sub_count < 0 || sub_begin + sub_count > n_sub ||
         (int64_t)hi_max * ny > field_stride) {
@@ -269,20 +308,52 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
         }
         ok = ok && dsts[0] != S;
         if (ok) {
+            // part (vk_diffuse_part): the interior of pass p is the rows whose inputs at
+            // the block's start are all owned -- [row_lo + 10 (p+1), row_hi - 10 (p+1)) on
+            // a side with halo rows -- and the edges are the rest of the pass's rows.
+            // The interior passes read and write only interior rows of each buffer, the
+            // edge passes read at most 20 rows into the interior of the pass before, which
+            // no later interior pass writes (it starts 10 rows deeper per pass), so all
+            // interior passes can run before any edge pass (while the halo arrives).
+            const bool halo_top = !edge_top && row_lo > lo_min, halo_bot = !edge_bot && row_hi < hi_max;
             for (int p = 0; p < P; ++p) {
                 const int e = sub_begin + 10 * p + 9;
                 const int grow = last_in_call - e;
                 const int lo = max(lo_min, row_lo - grow);
                 const int hi = min(hi_max, row_hi + grow);
-                const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
                 const double *f0 = (g_stencil_mode != 1 && ends_step && p == P - 1) ? field : nullptr;
-                launch_pass(10, s, p ? dsts[p - 1] : S, dsts[p], f0, n_fields, field_stride, ny, lo, hi, in_lo,
-                            in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr);
-                int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
-                if (rc) return rc;
+                const int ilo = halo_top ? row_lo + 10 * (p + 1) : lo;
+                const int ihi = halo_bot ? row_hi - 10 * (p + 1) : hi;
+                int ranges[3][2];
+                int nr = 0;
+                if (part == VK_PART_ALL) {
+                    ranges[nr][0] = lo, ranges[nr][1] = hi, ++nr;
+                } else if (part == VK_PART_INTERIOR) {
+                    ranges[nr][0] = ilo, ranges[nr][1] = ihi, ++nr;
+                } else {
+                    if (halo_top) ranges[nr][0] = lo, ranges[nr][1] = ilo, ++nr;
+                    if (halo_bot) ranges[nr][0] = ihi, ranges[nr][1] = hi, ++nr;
+                }
+                for (int q = 0; q < nr; ++q) {
+                    const int olo = ranges[q][0], ohi = ranges[q][1];
+                    if (olo >= ohi) continue;
+                    const int in_lo = max(lo_min, olo - 10), in_hi = min(hi_max, ohi + 10);
+                    launch_pass(10, s, p ? dsts[p - 1] : S, dsts[p], f0, n_fields, field_stride, ny, olo, ohi, in_lo,
+                                in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr);
+                    int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
+                    if (rc) return rc;
+                }
             }
             return VK_OK;
         }
+        if (part != VK_PART_ALL) {
+            vk::set_error("vk_diffuse_part: no 10-deep buffer plan for this block");
+            return VK_ERR_LIMIT;
+        }
+    }
+    if (part != VK_PART_ALL) {
+        vk::set_error("vk_diffuse_part: only the 10-deep plan splits");
+        return VK_ERR_LIMIT;
     }
     const std::vector<int> ks = odd_plan(sub_count);
     int j = sub_begin;

@@ -94,7 +94,9 @@ def make_halo_exchange(lat, rank: int, world: int, group=None):
 def make_uniform_allreduce(group=None):
     """Uniformity summary [lo0, hi0, lo1, hi1, ...] (vk_field_uniform) -> element-wise
     min of the lo entries and max of the hi entries over ranks (one all-reduce):
-    lo == hi afterwards iff every rank's band holds the same single value."""
+    lo == hi afterwards iff every rank's band holds the same single value.
+    ``group``: give it its own (``dist.new_group``) when the halo exchange runs
+    on another stream, so the two do not queue behind each other."""
 
     def allreduce(mm):
         t = mm.cpu() if _host_staged(mm.device, group) else mm

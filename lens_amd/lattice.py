@@ -173,8 +173,15 @@ class Lattice:
 
     def diffuse(self, timestep: float, halo_exchange: Optional[Callable] = None,
                 allreduce: Optional[Callable] = None, skip_uniform: bool = True, events=None,
-                before_final: Optional[Callable] = None, halo_ready: bool = False, summary=None):
+                before_final: Optional[Callable] = None, halo_ready: bool = False, summary=None,
+                halo_event=None):
         """Advance every plane by ``timestep`` (diffusion_field.py:385-407).
+
+        ``halo_event``: the first block's halo exchange was started on another
+        stream (:meth:`exchange_first_halo`) and this event marks its end: the
+        block's interior passes (rows that need no halo) run first, the launch
+        stream then waits for the event, and the edge passes finish the block
+        (vk_diffuse_part; the same bits as the whole block).
 
         ``summary`` (optional): the vk_field_uniform summary of the step-start planes,
         taken by the caller (the probe is then not run again).
@@ -202,10 +209,16 @@ class Lattice:
         lo_min = self.row_lo if self.edge_top else 0
         hi_max = self.row_hi if self.edge_bot else self.rows_local
         j = 0
+        if halo_event is not None:
+            halo_ready = True
         while j < n_sub:
             cnt = min(k, n_sub - j)
             if banded and not (halo_ready and j == 0):
                 halo_exchange(self.state_buffer(j), cnt)
+            if j == 0 and halo_event is not None:
+                self._run_block_overlapped(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, halo_event)
+                j += cnt
+                continue
             split = 0
             if before_final is not None and j + cnt == n_sub:
                 # unbanded: the planner's passes of [j, n_sub - 7) and [n_sub - 7, n_sub)
@@ -338,6 +351,30 @@ class Lattice:
         """Buffer holding the fields before substep j (vk_diffuse's rotation:
         field for j == 0, else work[(j-1) & 1])."""
         return self.fields if j == 0 else (self.work0 if ((j - 1) & 1) == 0 else self.work1)
+
+    def _run_part(self, j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, part):
+        """One part of a block (vk_diffuse_part); False if the block does not split."""
+        rc = native._lib.vk_diffuse_part(
+            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1),
+            len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, lo_min,
+            hi_max, int(self.edge_top), int(self.edge_bot), j, cnt, n_sub, coeff_dt,
+            native.ptr(mm), int(part), native.stream_handle())
+        if rc == native.VK_ERR_LIMIT:
+            return False
+        native.check(rc, 'vk_diffuse_part')
+        return True
+
+    def _run_block_overlapped(self, j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, halo_event):
+        """A block whose halo exchange is still in flight (``halo_event``): its
+        interior, then (after the event) its edges; the whole block after the
+        event if it does not split."""
+        main = torch.cuda.current_stream(self.device)
+        if not self._run_part(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, native.VK_PART_INTERIOR):
+            main.wait_event(halo_event)
+            self._run_block(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max)
+            return
+        main.wait_event(halo_event)
+        self._run_part(j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, native.VK_PART_EDGES)
 
     def _run_block(self, j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max):
         native.check(native._lib.vk_diffuse(

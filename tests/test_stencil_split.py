@@ -143,3 +143,69 @@ def test_split_pass_full_c4_planes(dev):
     ref = _run(dev, 20, 34, glc, second=ac, steps=2)
     got = _run(dev, 40, 0, glc, second=ac, steps=2)
     assert torch.equal(got.fields, ref.fields)
+
+
+@pytest.mark.parametrize('mode,variant', [('fma', 20), ('fma', 40), ('exact', 20)])
+@pytest.mark.parametrize('world,halo', [(2, 100), (3, 100), (3, 50)])
+def test_band_interior_then_edges_equals_whole_plane(dev, mode, variant, world, halo):
+    """vk_diffuse_part: a band's first block as its interior passes (no halo
+    needed: they run while the halo exchange is in flight) and then its edge
+    passes equals the whole plane bit for bit -- both arithmetic modes, the
+    pair-sum and the stage-split kernels, one and two halo blocks per step."""
+    from lens_amd import native
+    from lens_amd.distributed import row_bands
+    from lens_amd.lattice import Lattice, n_substeps
+    rng = np.random.default_rng(7)
+    nx, ny = 700, 203
+    f0 = rng.random((nx, ny)) * 5
+    g0 = np.full((nx, ny), 1.25)                    # a uniform plane: skipped in every part
+    with _kernel(variant, 0, mode=mode):
+        whole = Lattice(['a', 'b'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev,
+                        initial={'a': f0, 'b': g0})
+        whole.diffuse(1.0)
+        lats = [Lattice(['a', 'b'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, row_band=b,
+                        halo=halo, initial={'a': f0, 'b': g0}) for b in row_bands(nx, world)]
+        n_sub = n_substeps(1.0)
+        mms = []
+        for lat in lats:
+            mms.append(lat.uniform_summary(None).clone())
+        split = 0
+        j = 0
+        while j < n_sub:
+            cnt = min(halo, n_sub - j)
+            bufs = [lat.state_buffer(j) for lat in lats]
+            for r, lat in enumerate(lats):          # the halo exchange before the block
+                if not lat.edge_top:
+                    nb, src = lats[r - 1], bufs[r - 1]
+                    bufs[r][:, lat.row_lo - halo:lat.row_lo].copy_(src[:, nb.row_hi - halo:nb.row_hi])
+                if not lat.edge_bot:
+                    nb, src = lats[r + 1], bufs[r + 1]
+                    bufs[r][:, lat.row_hi:lat.row_hi + halo].copy_(src[:, nb.row_lo:nb.row_lo + halo])
+            for lat, mm in zip(lats, mms):
+                lo_min = lat.row_lo if lat.edge_top else 0
+                hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
+                coef = lat.diffusion * 0.01
+                if j == 0 and lat._run_part(j, cnt, n_sub, coef, mm, lo_min, hi_max, native.VK_PART_INTERIOR):
+                    split += 1
+                    assert lat._run_part(j, cnt, n_sub, coef, mm, lo_min, hi_max, native.VK_PART_EDGES)
+                else:
+                    lat._run_block(j, cnt, n_sub, coef, mm, lo_min, hi_max)
+            j += cnt
+        torch.cuda.synchronize()
+    assert split == world                           # every band's first block split
+    got = torch.cat([lat.owned() for lat in lats], 1).cpu().numpy()
+    assert np.array_equal(got, whole.owned().cpu().numpy()), (world, halo)
+
+
+def test_part_refuses_blocks_it_cannot_split(dev):
+    """The whole plane (no halo rows) and the odd-depth plan do not split:
+    VK_ERR_LIMIT, nothing launched, the field unchanged."""
+    from lens_amd import native
+    from lens_amd.lattice import Lattice
+    f0 = np.random.default_rng(1).random((64, 64))
+    with _kernel(20, 0):
+        lat = Lattice(['a'], (64, 64), (64.0, 64.0), 10.0, 5.0, device=dev, initial={'a': f0})
+        mm = lat.uniform_summary(None)
+        assert not lat._run_part(0, 100, 100, 0.05, mm, 0, 64, native.VK_PART_INTERIOR)
+    torch.cuda.synchronize()
+    assert np.array_equal(lat.owned('a').cpu().numpy(), f0)
