@@ -8,6 +8,13 @@ tiles, variant 20, depth 10, tolerance mode), and each band is reported against
 
     python scripts/rank_emulate.py N halo rows [variant depth [mode]]     (mode: exact | fma)
     python scripts/rank_emulate.py N --sweep halo:rows:variant:depth,...  (tolerance mode)
+
+XFER_US (env, default 0): the stand-in exchange also holds its stream for that
+long (torch.cuda._sleep, calibrated), standing in for the RCCL transfer over xGMI
+(~6.5 MB per neighbour and step at h = 100: ~100 us at ~65 GB/s).  Each band
+case is then timed twice: the exchange before the block on the launch stream
+(serial), and on a side stream beside the block's interior passes, the edge
+passes after it (overlap, Lattice.diffuse(halo_event=...)).
 """
 import json
 import os
@@ -46,7 +53,27 @@ def whole_plane_ms(variant=20, depth=10, rows=34):
     return ms
 
 
-def band_ms(world, halo, rows, variant, depth):
+XFER_US = float(os.environ.get('XFER_US', '0'))
+_CYCLES_PER_US = None
+
+
+def _sleep_us(us):
+    """Hold the current stream for ~us microseconds (calibrated spin kernel)."""
+    global _CYCLES_PER_US
+    if us <= 0:
+        return
+    if _CYCLES_PER_US is None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000000)
+        e0.record()
+        torch.cuda._sleep(10000000)
+        e1.record()
+        torch.cuda.synchronize()
+        _CYCLES_PER_US = 10000000 / (e0.elapsed_time(e1) * 1e3)
+    torch.cuda._sleep(int(us * _CYCLES_PER_US))
+
+
+def band_ms(world, halo, rows, variant, depth, overlap=False):
     band = row_bands(nx, world)[1 if world > 2 else 0]
     glc = configs.gaussian_bump_field((nx, nx))
     lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (4096.0, 4096.0), 10.0, 5.0, device=dev, row_band=band,
@@ -57,6 +84,7 @@ def band_ms(world, halo, rows, variant, depth):
     bufs = [torch.empty((2, h, nx), dtype=torch.float64, device=dev) for _ in range(4)]
 
     def fake_exchange(src, cnt):
+        _sleep_us(XFER_US)
         if not lat.edge_top:
             bufs[0].copy_(src[:, lat.row_lo:lat.row_lo + h]); bufs[1].copy_(bufs[0])
             src[:, lat.row_lo - h:lat.row_lo].copy_(bufs[1])
@@ -64,17 +92,26 @@ def band_ms(world, halo, rows, variant, depth):
             bufs[2].copy_(src[:, lat.row_hi - h:lat.row_hi]); bufs[3].copy_(bufs[2])
             src[:, lat.row_hi:lat.row_hi + h].copy_(bufs[3])
 
-    ms = time_steps(lambda: lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None))
+    side = torch.cuda.Stream(device=dev)
+
+    def one_step():
+        if overlap:
+            done = lat.exchange_first_halo(1.0, fake_exchange, side)
+            lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None, halo_event=done)
+        else:
+            lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
+
+    ms = time_steps(one_step)
     # the same step with its launch sequence replayed from one HIP graph (the stand-in
     # exchange included), as the bench replays a band's halo blocks: the GPU's time
     # without the host's issue of ~20 launches per step
-    lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
+    one_step()
     torch.cuda.synchronize()
     s = torch.cuda.Stream(device=dev)
     s.wait_stream(torch.cuda.current_stream(dev))
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s), torch.cuda.graph(g, stream=s):
-        lat.diffuse(1.0, halo_exchange=fake_exchange, allreduce=lambda mm: None)
+        one_step()
     torch.cuda.current_stream(dev).wait_stream(s)
     g.replay()
     graph_ms = time_steps(g.replay)
@@ -96,11 +133,13 @@ def main():
                       flush=True)
         for spec in sys.argv[3].split(','):
             halo, rows, variant, depth = (int(x) for x in spec.split(':'))
-            band, ms, graph_ms = band_ms(world, halo, rows, variant, depth)
-            print(json.dumps({'world': world, 'band': list(band), 'halo': halo, 'rows': rows, 'variant': variant,
-                              'depth': depth, 'ms_per_step': round(ms, 4),
-                              'efficiency': round(whole / world / ms, 3), 'graph_ms_per_step': round(graph_ms, 4),
-                              'graph_efficiency': round(whole / world / graph_ms, 3)}), flush=True)
+            for overlap in ((False, True) if XFER_US > 0 else (False,)):
+                band, ms, graph_ms = band_ms(world, halo, rows, variant, depth, overlap)
+                print(json.dumps({'world': world, 'band': list(band), 'halo': halo, 'rows': rows, 'variant': variant,
+                                  'depth': depth, 'xfer_us': XFER_US, 'overlap': overlap,
+                                  'ms_per_step': round(ms, 4), 'efficiency': round(whole / world / ms, 3),
+                                  'graph_ms_per_step': round(graph_ms, 4),
+                                  'graph_efficiency': round(whole / world / graph_ms, 3)}), flush=True)
         return
     halo, rows = int(sys.argv[2]), int(sys.argv[3])
     variant = int(sys.argv[4]) if len(sys.argv) > 4 else 20
