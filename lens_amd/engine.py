@@ -48,6 +48,7 @@ from typing import Dict, List, Tuple
 
 import numpy as np
 
+from lens_amd.agent_store import AgentsNode, AgentView
 from lens_amd.division import DIVIDERS
 from lens_amd.process import deep_merge
 from lens_amd.registry import DeviceField, make_update_field_with_exchange
@@ -153,6 +154,15 @@ class Experiment:
         self.invoke = config.get('invoke') or _InvokeNow
         self.avogadro = config.get('avogadro', N_A_LEGACY)
         self.state = _copy_tree(config.get('initial_state', {}))
+        # config['agent_columns'] = ('agents',): the agents under that node live in
+        # columns (lens_amd.agent_store) -- per-agent dicts become views of rows, and
+        # batched processes read and write whole columns (_schedule, _apply_group)
+        self.agent_columns = normalize_path(config['agent_columns']) if config.get('agent_columns') else None
+        if self.agent_columns is not None:
+            node = self.state
+            for k in self.agent_columns[:-1]:
+                node = node.setdefault(k, {})
+            node[self.agent_columns[-1]] = AgentsNode(node.get(self.agent_columns[-1]) or {})
         self.schema: Dict[Tuple, str] = {}
         self._globs: List[Tuple] = []            # the schema paths holding a '*'
         self._port_paths: Dict[Tuple, Tuple] = {}
@@ -662,6 +672,8 @@ class Experiment:
             self.apply_update(up.as_dict(), proc_path)
             return
         apath = ppath + (key,)
+        if isinstance(agents, AgentsNode) and self._apply_leaves_columns(agents, apath, up):
+            return
         updaters, keys, path = self.updaters, up.keys, up.path
         leaf_updaters = self._leaf_updaters
         by_agent = self._agent_leaf_names.get((apath, path))
@@ -716,9 +728,236 @@ class Experiment:
                 if type(new) is dict:
                     self._version += 1
 
+    # -- columnar agents: whole-column application (lens_amd.agent_store) ---------------
+    def _all_agents_resolve(self, apath, agents, leaf, name):
+        """Whether every agent's ``leaf`` (a path below the agent) resolves to the
+        schema updater ``name`` -- checked once per structure version."""
+        cache = self.__dict__.setdefault('_resolve_cache', {})
+        key = (apath, leaf, name)
+        ent = cache.get(key)
+        if ent is None or ent[0] != self._version:
+            ok = all(self._updater_at(apath + (aid,) + leaf) == name for aid in agents)
+            ent = cache[key] = (self._version, ok)
+        return ent[1]
+
+    def _apply_leaves_columns(self, agents, apath, up):
+        """An AgentLeafUpdate on columnar agents as one column write per key, when
+        that is what the per-agent walk would do: every agent present with the
+        branch and every leaf a float that its schema sets (``set``).  False:
+        nothing applied (the per-agent walk follows)."""
+        from lens_amd.agent_store import _F
+        t = agents.table
+        cache = self.__dict__.get('_leaf_rows')
+        if cache is not None and cache[0] is agents and cache[1] == self._version and cache[2] == up.ids:
+            rows = cache[3]
+        else:
+            try:
+                rows = agents.rows(up.ids)
+            except KeyError:
+                return False
+            self._leaf_rows = (agents, self._version, list(up.ids), rows)
+        path = up.path
+        for i in range(1, len(path) + 1):
+            m = t.present.get(path[:i])
+            if m is None or not m[rows].all():
+                return False
+        leaves = []
+        for k in up.keys:
+            lp = path + (k,)
+            if t.kind.get(lp) != _F or not t.present[lp][rows].all():
+                return False
+            if not self._all_agents_resolve(apath, agents, lp, 'set'):
+                return False
+            leaves.append(lp)
+        vals = np.asarray(up.rows, dtype=np.float64).reshape(len(up.ids), len(leaves))
+        if len(set(up.ids)) != len(up.ids):
+            return False
+        for j, lp in enumerate(leaves):
+            t.cols[lp][rows] = vals[:, j]
+            t.npf[lp][rows] = False                      # the row values are Python floats
+        return True
+
+    def _schedule(self, processes, front):
+        """The scheduler's entries for ``processes`` (walk order): a run of two or
+        more consecutive agent kinetics processes that can be applied as columns
+        (:meth:`_kinetics_group`) becomes one group entry with one front; every
+        other process is its own entry.  Only processes without a front yet are
+        grouped (the caller builds groups at the start of an update call)."""
+        sched = []
+        run = []
+
+        def close():
+            if len(run) >= 2 and all(front.get(p) is None for p, _, _ in run):
+                grp = self._kinetics_group(run)
+                if grp is not None:
+                    sched.append(grp)
+                    run.clear()
+                    return
+            for p, proc, _ in run:
+                sched.append((p, proc))
+            run.clear()
+
+        can = self.agent_columns is not None and hasattr(self.invoke, 'group_call')
+        for path, proc in processes:
+            key = self._group_key(path, proc) if can else None
+            if key is None or (run and key != run[0][2]):
+                close()
+            if key is None:
+                sched.append((path, proc))
+            else:
+                run.append((path, proc, key))
+        close()
+        return sched
+
+    def _group_key(self, path, proc):
+        from lens_amd.process import BatchedConvenienceKinetics
+        if not isinstance(proc, BatchedConvenienceKinetics) or len(path) != len(self.agent_columns) + 2 or \
+                path[:len(self.agent_columns)] != self.agent_columns:
+            return None
+        topo = self._topology_of(path)
+        p = proc.parameters
+        return (type(proc), proc.signature, path[-1], proc.local_timestep(), p.get('integrator', 'euler'),
+                p.get('rtol', 1e-8), p.get('atol', 1e-12), p.get('max_steps', 100000),
+                tuple(sorted((k, tuple(v)) for k, v in topo.items())))
+
+    def _kinetics_group(self, run):
+        """A group entry for a run of agent kinetics processes, or None if any
+        member's outputs would not land as whole-column writes.  The members'
+        per-agent plans (:meth:`_kinetics_plan`) must all be the same plan in
+        column terms: every output a float leaf of the agent's own row with the same
+        updater, every exchange on the same device fields."""
+        from lens_amd.agent_store import _F
+        agents = self.get(self.agent_columns)
+        if not isinstance(agents, AgentsNode):
+            return None
+        t = agents.table
+        procs = [proc for _, proc, _ in run]
+        paths = [p for p, _, _ in run]
+        aids = [p[len(self.agent_columns)] for p in paths]
+        try:
+            rows = agents.rows(aids)
+        except KeyError:
+            return None
+        shape = None
+        for path, proc, aid in zip(paths, procs, aids):
+            plan = self._kinetics_plan(path, proc)
+            if plan is None:
+                return None
+            dyn, flux, fields, exch, states, site = plan
+            if site is None:
+                return None
+            row = agents.row(aid)
+            cols = []
+            for tgt in list(dyn) + list(flux):
+                if tgt is None:
+                    return None                     # a skipped output: the per-agent path decides
+                node, k, fn, kind = tgt
+                if not isinstance(node, AgentView) or node._r != row or kind == 2:
+                    return None
+                cols.append((node._p + (k,), kind))
+            fl = []
+            for ft in fields:
+                if ft is None:
+                    fl.append(None)
+                    continue
+                fnode, mol = ft
+                if isinstance(fnode, AgentView):
+                    return None
+                fl.append((id(fnode), mol))
+            loc = states.get('global')
+            if not isinstance(loc, AgentView) or loc._r != row:
+                return None
+            sig = (tuple(cols), tuple(fl), id(states.get('dimensions')), loc._p)
+            if shape is None:
+                shape = sig
+                first_plan = plan
+            elif sig != shape:
+                return None
+        dyn_cols, fields = shape[0][:len(first_plan[0])], first_plan[2]
+        flux_cols = shape[0][len(first_plan[0]):]
+        for c, _ in shape[0]:
+            if t.kind.get(c) != _F:
+                return None
+        topo = self._topology_of(paths[0])
+        pack = []
+        for port, name in procs[0].table.species:
+            rel = topo.get(port)
+            pack.append(None if rel is None else normalize_path(tuple(rel)) + (name,))
+        gl = topo.get('global')
+        if gl is None or any(r is not None and r[:1] == ('..',) for r in pack):
+            return None
+        return _Group(key=('__group__', paths[0], paths[-1], len(paths)), paths=paths, procs=procs, aids=aids,
+                      rows=rows, table=t, pack=pack, m2c=normalize_path(tuple(gl)) + ('mmol_to_counts',),
+                      loc=shape[3] + ('location',), dyn=dyn_cols, flux=flux_cols, fields=fields,
+                      dims=first_plan[4]['dimensions'], exch=first_plan[3], version=self._version,
+                      params=np.stack([p.param_values for p in procs], axis=1),
+                      timestep=procs[0].local_timestep())
+
+    def _invoke_group(self, g, timestep):
+        """Pack the group's agents from the columns (the values pack_state reads
+        per agent) and hand them to the invoke hook as one call."""
+        t, rows = g.table, g.rows
+        conc = np.empty((len(g.pack), len(rows)), dtype=np.float64)
+        for i, c in enumerate(g.pack):
+            conc[i] = 0.0 if c is None else t.gather(c, rows, 0.0)
+        m = t.present.get(g.m2c)
+        if m is None or not m[rows].all():
+            raise KeyError('mmol_to_counts')
+        m2c = t.gather(g.m2c, rows)
+        return self.invoke.group_call(g.procs, timestep, conc, m2c, g.params)
+
+    def _apply_group(self, g, flux, delta, counts):
+        """A group's kinetics outputs as column writes -- each agent's
+        :meth:`_apply_kinetics` in agent order: internal deltas, fluxes, then the
+        exchange queued on the device fields."""
+        from lens_amd.agent_store import _F
+        t, rows = g.table, g.rows
+        if any(t.kind.get(c) != _F for c, _ in g.dyn + g.flux) or self._version != g.version:
+            for i, (path, proc) in enumerate(zip(g.paths, g.procs)):
+                self._apply_kinetics(path, proc, flux[:, i].tolist(), delta[:, i].tolist(),
+                                     counts[:, i].tolist())
+            return
+        for (c, kind), d in zip(g.dyn, delta):
+            col = t.cols[c]
+            if kind == 0:
+                col[rows] = col[rows] + d                 # float + float, or np.float64 + float
+            else:
+                col[rows] = d
+                t.npf[c][rows] = False
+        for (c, kind), f in zip(g.flux, flux):
+            col = t.cols[c]
+            col[rows] = col[rows] + f if kind == 0 else f
+            t.npf[c][rows] = True                         # np.float64(f) (+ ...) in the per-agent path
+        if not any(ft is not None for ft in g.fields):
+            return
+        loc = np.array([t.cols[g.loc][r] for r in rows.tolist()], dtype=np.float64).reshape(len(rows), 2)
+        dims = g.dims
+        nx, ny = int(dims['n_bins'][0]), int(dims['n_bins'][1])
+        i = np.mod(np.floor(loc[:, 0] * nx / dims['bounds'][0]).astype(np.int64), nx)
+        j = np.mod(np.floor(loc[:, 1] * ny / dims['bounds'][1]).astype(np.int64), ny)
+        bins = (i * ny + j).tolist()
+        _, bva, shape = g.exch.site({'global': {'location': [0.0, 0.0]}, 'dimensions': dims})
+        for e, ft in enumerate(g.fields):
+            if ft is None:
+                continue
+            fnode, mol = ft
+            cur = fnode[mol]
+            if type(cur) is not DeviceField:
+                for a in range(len(rows)):          # a host field: the updater, agent by agent
+                    states = {'global': {'location': loc[a].tolist()}, 'dimensions': dims}
+                    cur = fnode[mol] = g.exch(fnode[mol], int(counts[e, a]), states)
+                continue
+            if cur._t.shape != shape:
+                raise ValueError('field shape %s does not match n_bins %s' % (cur.shape, list(shape)))
+            cur.queue_exchange_many(bins, counts[e], bva)
+
     def send_updates(self, updates, derivers=None):
         self._deleted = {}
         for update, path in updates:
+            group = getattr(update, 'group_raw', None)
+            if group is not None:
+                self._apply_group(path, *group())
+                continue
             raw = getattr(update, 'raw', None)
             leaves = getattr(update, 'leaf_raw', None)
             if raw is not None:
@@ -787,17 +1026,54 @@ class Experiment:
         # _generate / _divide update can add processes; here it is walked again only
         # after such an update moved the structure
         seen = None
+        sched = None
         while time < interval:
             if seen != self._structure:
-                seen = self._structure
                 everything = self._walk(self.processes, ())
                 processes = [(p, s) for p, s in everything if not s.is_deriver()]
                 derivers = [(p, s) for p, s in everything if s.is_deriver()]
+                if seen is None:
+                    # columnar agents: runs of agent kinetics processes are scheduled as one
+                    # entry each (one front, one invoke, one column apply), formed only here,
+                    # at the start of the call, where every front starts at 0 -- and kept for
+                    # the next call while the process list and the store's structure stand
+                    cache = self.__dict__.get('_sched_cache')
+                    if (cache is not None and cache[0] == self._structure and cache[1] == self._version and
+                            cache[2] == processes):
+                        sched = cache[3]
+                    else:
+                        sched = self._schedule(processes, front)
+                        self._sched_cache = (self._structure, self._version, processes, sched)
+                else:
+                    # the structure moved mid-call: groups dissolve into their members, in
+                    # place in the front order, with the group's front (and a pending update
+                    # split per member); no regrouping until the next call
+                    front = _dissolve_groups(front)
+                    sched = processes
+                seen = self._structure
                 live = {p for p, _ in processes}
-                front = {p: f for p, f in front.items() if p in live}
+                front = {p: f for p, f in front.items() if p in live or type(p[0]) is str and p[0] == '__group__'}
             full_step = INFINITY
             invoke, states_of = self.invoke, self.process_states
-            for path, proc in processes:
+            last = None
+            for entry in sched:
+                if type(entry) is _Group:
+                    key = entry.key
+                    adv = front.get(key)
+                    if adv is None:
+                        adv = front[key] = {'time': time, 'update': None, 'group': entry}
+                    process_time = adv['time']
+                    if process_time <= time:
+                        future = min(process_time + entry.timestep, interval)
+                        timestep = future - process_time
+                        pending = self._invoke_group(entry, timestep)
+                        if timestep < full_step:
+                            full_step = timestep
+                        adv['time'] = future
+                        adv['update'] = (pending, entry)
+                    last = key
+                    continue
+                path, proc = entry
                 adv = front.get(path)
                 if adv is None:
                     adv = front[path] = {'time': time, 'update': None}
@@ -810,11 +1086,12 @@ class Experiment:
                         full_step = timestep
                     adv['time'] = future
                     adv['update'] = (pending, path)
+                last = path
             if full_step == INFINITY:
                 next_event = interval
                 for _ in front.keys():
-                    if front[path]['time'] < next_event:   # the reference's stale `path` (:1414-1419)
-                        next_event = front[path]['time']
+                    if front[last]['time'] < next_event:   # the reference's stale `path` (:1414-1419)
+                        next_event = front[last]['time']
                 time = next_event
             else:
                 future = time + full_step
@@ -827,6 +1104,44 @@ class Experiment:
                 time = future
                 self.local_time += full_step
         return self
+
+
+class _Group:
+    """A scheduler entry for a run of agent kinetics processes handled as columns."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+class _MemberUpdate:
+    """Member i of a group's pending update, as a per-agent future (``raw()``)."""
+
+    def __init__(self, pending, i, proc):
+        self.pending, self.i, self.proc = pending, i, proc
+
+    def raw(self):
+        flux, delta, counts = self.pending.group_raw()
+        i = self.i
+        return self.proc, flux[:, i].tolist(), delta[:, i].tolist(), counts[:, i].tolist()
+
+    def get(self, timeout=0):
+        return self.proc.unpack_update(*self.raw()[1:])
+
+
+def _dissolve_groups(front):
+    """Front entries with every group replaced by its members' entries, in place
+    in the order (a group's pending update split into per-member futures)."""
+    out = {}
+    for key, adv in front.items():
+        g = adv.get('group') if isinstance(adv, dict) else None
+        if g is None:
+            out[key] = adv
+            continue
+        upd = adv['update']
+        for i, (path, proc) in enumerate(zip(g.paths, g.procs)):
+            out[path] = {'time': adv['time'],
+                         'update': (_MemberUpdate(upd[0], i, proc), path) if upd is not None else None}
+    return out
 
 
 def _copy_tree(t):

@@ -85,6 +85,58 @@ def _run_group(items: List[_Packed], device=None, raw: bool = False) -> List:
     return [it.process.unpack_update(f, d, c) for it, f, d, c in zip(items, flux_l, delta_l, counts_l)]
 
 
+def _run_arrays(procs, interval, conc, m2c, params, device=None):
+    """One launch for a group of agents given as arrays (conc [species, n], m2c
+    [n], params [P, n]): what _run_group computes from per-agent packs, returned
+    as host arrays (flux [R, n], delta [ND, n], counts [E, n])."""
+    p0 = procs[0]
+    t = p0.table
+    eng = engine_for(p0, device)
+    n = len(procs)
+    dev = eng.device
+    conc_d = torch.from_numpy(np.ascontiguousarray(conc)).to(dev)
+    params_d = torch.from_numpy(np.ascontiguousarray(params)).to(dev)
+    m2c_d = torch.from_numpy(np.ascontiguousarray(m2c)).to(dev)
+    delta = torch.zeros((t.n_dyn, n), dtype=torch.float64, device=dev)
+    integrator = p0.parameters.get('integrator', 'euler')
+    if integrator == 'euler':
+        flux, counts, status = eng.euler(interval, params_d, conc_d, m2c_d, delta=delta)
+    elif integrator == 'dopri5':
+        h = torch.tensor([getattr(p, '_h_state', 0.0) for p in procs], dtype=torch.float64, device=dev)
+        flux, counts, status, _ = eng.dopri5(
+            interval, params_d, conc_d, m2c_d, h_state=h, delta=delta,
+            rtol=p0.parameters.get('rtol', 1e-8), atol=p0.parameters.get('atol', 1e-12),
+            max_steps=p0.parameters.get('max_steps', 100000))
+        for p, hv in zip(procs, h.cpu().tolist()):
+            p._h_state = hv
+    else:
+        raise ValueError('unknown integrator %r' % integrator)
+    st = status.cpu().numpy()
+    if st.any():
+        bad = int(np.flatnonzero(st)[0])
+        raise FloatingPointError('agent %d: kernel status %d (1=max steps, 2=step underflow, '
+                                 '4=non-finite)' % (bad, int(st[bad])))
+    return flux.cpu().numpy(), delta.cpu().numpy(), counts.cpu().numpy()
+
+
+class _GroupFuture:
+    """A group call's outputs (lens_amd.engine.Experiment's columnar agents):
+    ``group_raw()`` = (flux [R, n], delta [ND, n], counts [E, n]) host arrays."""
+    __slots__ = ('owner', 'result')
+
+    def __init__(self, owner):
+        self.owner = owner
+        self.result = None
+
+    def group_raw(self):
+        if self.result is None:
+            self.owner.flush()
+        return self.result
+
+    def get(self, timeout=0):
+        raise TypeError('a group call has no single update dict (use group_raw)')
+
+
 def run_batch(calls, device=None) -> List[dict]:
     """Evaluate [(process, interval, states)] in as few launches as possible."""
     packed = [_Packed(p, dt, s) for p, dt, s in calls]
@@ -151,6 +203,7 @@ class BatchedInvoke:
     def __init__(self, device=None):
         self.device = device
         self._pending = []
+        self._groups = []
 
     def __call__(self, process, interval, states):
         if not isinstance(process, BatchedConvenienceKinetics):
@@ -162,9 +215,20 @@ class BatchedInvoke:
         self._pending.append((fut, _Packed(process, interval, states)))
         return fut
 
+    def group_call(self, procs, interval, conc, m2c, params):
+        """Record a whole group of agents' calls, packed as arrays by the caller
+        (lens_amd.engine.Experiment with columnar agents); launched with the
+        step's other calls at the first ``get()``."""
+        fut = _GroupFuture(self)
+        self._groups.append((fut, procs, float(interval), conc, m2c, params))
+        return fut
+
     def flush(self):
         """Launch every recorded call: one kernel per (network, interval,
         integrator) group; each future receives its agent's outputs."""
+        groups, self._groups = self._groups, []
+        for fut, procs, interval, conc, m2c, params in groups:
+            fut.result = _run_arrays(procs, interval, conc, m2c, params, self.device)
         if not self._pending:
             return
         pending, self._pending = self._pending, []

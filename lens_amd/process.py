@@ -343,8 +343,10 @@ class BatchedDiffusionField(ProcessBase):
                 # diffusion_field.py:362-379): one vk_gather, one host copy
                 ids = list(agents)
                 n = len(ids)
-                bins = torch.from_numpy(_bin_sites([agents[a]['boundary']['location'] for a in ids], self.n_bins,
-                                                   self.bounds).astype(np.int32)).to(self.device)
+                values_at = getattr(agents, 'values_at', None)      # columnar agents: one column read
+                locs = (values_at(('boundary', 'location'), ids) if values_at is not None else
+                        [agents[a]['boundary']['location'] for a in ids])
+                bins = torch.from_numpy(_bin_sites(locs, self.n_bins, self.bounds).astype(np.int32)).to(self.device)
                 vals = torch.empty((len(self.molecule_ids), n), dtype=torch.float64, device=self.device)
                 native.check(native._lib.vk_gather(
                     native.ptr(lat.fields), lat.field_stride, native.ptr(bins), n, native.ptr(self._map),

@@ -83,6 +83,14 @@ class DeviceField:
         self._bins.append(bin_lin)
         self._counts.append(count)
 
+    def queue_exchange_many(self, bins, counts, binvol_avogadro: float):
+        """:meth:`queue_exchange` for several calls at once, in list order."""
+        if self._bva is not None and binvol_avogadro != self._bva:
+            self.flush()
+        self._bva = binvol_avogadro
+        self._bins.extend(bins)
+        self._counts.extend(np.asarray(counts, dtype=np.int64).tolist())
+
     @property
     def pending(self) -> int:
         return len(self._bins)

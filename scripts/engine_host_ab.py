@@ -41,16 +41,24 @@ class StubInvoke(BatchedInvoke):
         super().__init__(None)
         self.rng = np.random.default_rng(3)
 
-    def flush(self):
-        pending, self._pending = self._pending, []
+    def _pool(self, table):
         pool = self.__dict__.get('pool')
         if pool is None:     # 64 seeded outputs, reused in turn (the stand-in costs next to nothing)
-            t = pending[0][1].process.table
-            pool = self.pool = [(self.rng.normal(size=t.n_reactions).tolist(),
-                                 (1e-3 * self.rng.normal(size=t.n_dyn)).tolist(),
-                                 self.rng.integers(-50, 50, size=t.n_ext).tolist()) for _ in range(64)]
+            pool = self.pool = [(self.rng.normal(size=table.n_reactions).tolist(),
+                                 (1e-3 * self.rng.normal(size=table.n_dyn)).tolist(),
+                                 self.rng.integers(-50, 50, size=table.n_ext).tolist()) for _ in range(64)]
+        return pool
+
+    def flush(self):
+        pending, self._pending = self._pending, []
+        groups, self._groups = self._groups, []
         for i, (fut, it) in enumerate(pending):
-            fut.result = (it.process,) + pool[i & 63]
+            fut.result = (it.process,) + self._pool(it.process.table)[i & 63]
+        for fut, procs, interval, conc, m2c, params in groups:     # columnar agents: agent i = call i
+            pool = self._pool(procs[0].table)
+            sel = [pool[i & 63] for i in range(len(procs))]
+            fut.result = (np.array([x[0] for x in sel]).T.copy(), np.array([x[1] for x in sel]).T.copy(),
+                          np.array([x[2] for x in sel], dtype=np.int64).T.copy())
 
 
 class StubDiffusion(Process):
@@ -107,15 +115,37 @@ def build(n):
     return processes, topology, init
 
 
-def main():
+def make(n, columns):
     from lens_amd.engine import Experiment
+    p, t, init = build(n)
+    cfg = {'processes': p, 'topology': t, 'initial_state': init, 'invoke': StubInvoke()}
+    if columns:
+        cfg['agent_columns'] = ('agents',)
+    exp = Experiment(cfg)
+    for m in list(exp.state['fields']):      # after the initial state's copy (it clones device fields)
+        exp.state['fields'][m] = host_field()
+    return exp
+
+
+def main():
+    """COLUMNS=1: the agents held in columns (lens_amd.agent_store); COLUMNS=both:
+    both stores, and their states after the timed calls must be equal."""
+    from lens_amd.engine import Experiment  # noqa: F401
     sizes = [int(x) for x in sys.argv[1:]] or [500, 2000, 8000, 32000]
     reps = int(os.environ.get('REPS', '5'))
+    mode = os.environ.get('COLUMNS', '0')
     for n in sizes:
-        p, t, init = build(n)
-        exp = Experiment({'processes': p, 'topology': t, 'initial_state': init, 'invoke': StubInvoke()})
-        for m in list(exp.state['fields']):      # after the initial state's copy (it clones device fields)
-            exp.state['fields'][m] = host_field()
+        if mode == 'both':
+            a, b = make(n, False), make(n, True)
+            for _ in range(3):
+                a.update(1.0)
+                b.update(1.0)
+            fa = [list(f._bins) + list(f._counts) for f in a.state['fields'].values()]
+            fb = [list(f._bins) + list(f._counts) for f in b.state['fields'].values()]
+            same = repr(a.state['agents']) == repr(b.state['agents']) and fa == fb
+            print('agents %6d  dict store == columns: %s' % (n, same), flush=True)
+            continue
+        exp = make(n, mode == '1')
         exp.update(1.0)
         best = float('inf')
         for _ in range(reps):
@@ -123,8 +153,8 @@ def main():
             t0 = time.process_time()          # this process's CPU time: steadier than wall time on a shared host
             exp.update(3.0)
             best = min(best, time.process_time() - t0)
-        print('agents %6d  %.2f us of CPU per agent-step (min of %d calls of 3 steps)'
-              % (n, best / (3 * n) * 1e6, reps), flush=True)
+        print('agents %6d  %.2f us of CPU per agent-step (min of %d calls of 3 steps)%s'
+              % (n, best / (3 * n) * 1e6, reps, '  [columns]' if mode == '1' else ''), flush=True)
 
 
 if __name__ == '__main__':

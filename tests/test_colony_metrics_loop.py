@@ -43,7 +43,7 @@ def single_agent_config(location):
                          'width': width, 'mass': 1339.0, 'thrust': 0, 'torque': 0}}
 
 
-def colony_metrics_experiment(invoke=None):
+def colony_metrics_experiment(invoke=None, columns=False):
     random.seed(1)
     np.random.seed(1)
     ids = ['0', '1']
@@ -56,11 +56,13 @@ def colony_metrics_experiment(invoke=None):
     config = {'processes': processes, 'topology': topology, 'initial_state': initial}
     if invoke is not None:
         config['invoke'] = invoke
+    if columns:
+        config['agent_columns'] = ('agents',)
     return Experiment(config)
 
 
-def run_csv(tmp_path, invoke=None, steps=2400):
-    exp = colony_metrics_experiment(invoke)
+def run_csv(tmp_path, invoke=None, steps=2400, columns=False):
+    exp = colony_metrics_experiment(invoke, columns)
     em = ExperimentEmitter(exp, extra={'dimensions': {'depth': 3000.0}})
     em.emit()
     for _ in range(steps):
@@ -86,8 +88,10 @@ def assert_same_csv(got, want):
     assert got == want
 
 
-def test_process_api_loop_rebuilds_colony_metrics_csv_byte_for_byte(tmp_path):
-    got, exp = run_csv(tmp_path)
+@pytest.mark.parametrize('columns', [False, True])
+def test_process_api_loop_rebuilds_colony_metrics_csv_byte_for_byte(tmp_path, columns):
+    """Per-agent dicts, and agents held in columns (lens_amd.agent_store)."""
+    got, exp = run_csv(tmp_path, columns=columns)
     want = gzip.open(os.path.join(GOLDEN, 'colony_metrics.csv.gz'), 'rb').read()
     assert_same_csv(got, want)
     assert len(exp.state['agents']) > 2                  # the colony divided

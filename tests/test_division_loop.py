@@ -69,8 +69,10 @@ def run(kind, intervals, seed=11):
     np.random.seed(seed)
     random.seed(seed)
     p, t, init = colony()
-    exp = Experiment({'processes': p, 'topology': t, 'initial_state': init}) if kind == 'engine' else \
-        OracleExperiment(p, t, init)
+    cfg = {'processes': p, 'topology': t, 'initial_state': init}
+    if kind == 'columns':                     # the agents held in columns (lens_amd.agent_store)
+        cfg['agent_columns'] = ('agents',)
+    exp = Experiment(cfg) if kind in ('engine', 'columns') else OracleExperiment(p, t, init)
     snaps = []
     for interval in intervals:
         exp.update(interval)
@@ -82,8 +84,9 @@ def run(kind, intervals, seed=11):
 INTERVALS = (1.0, 2.0, 0.5, 3.5, 4.0, 1.0, 6.0)
 
 
-def test_division_ids_order_and_states_equal_reference_loop():
-    got, eng = run('engine', INTERVALS)
+@pytest.mark.parametrize('kind', ['engine', 'columns'])
+def test_division_ids_order_and_states_equal_reference_loop(kind):
+    got, eng = run(kind, INTERVALS)
     ref, orc = run('oracle', INTERVALS)
     assert len(got) == len(ref)
     for k, (g, r) in enumerate(zip(got, ref)):

@@ -43,7 +43,7 @@ class EnzymeExpression:
         return {'internal': {'EIIglc': self.rate * timestep * (1.0 + states['internal']['EIIglc'])}}
 
 
-def _colony(batched, dev):
+def _colony(batched, dev, expression=True):
     from lens_amd import configs
     from lens_amd.process import BatchedConvenienceKinetics, BatchedDiffusionField
     from oracle.experiment import OracleConvenienceKinetics, OracleDiffusionField
@@ -65,12 +65,14 @@ def _colony(batched, dev):
         kin_cfg = dict(cfg, time_step=1.0)
         kin = BatchedConvenienceKinetics(kin_cfg) if batched else OracleConvenienceKinetics(kin_cfg)
         aid = 'a%02d' % a
-        processes['agents'][aid] = {'kinetics': kin, 'expression': EnzymeExpression(1e-4 * (1 + a % 3), 2.0)}
+        processes['agents'][aid] = {'kinetics': kin}
         topology['agents'][aid] = {
             'kinetics': {'internal': ('internal',), 'external': ('boundary', 'external'), 'fluxes': ('fluxes',),
                          'fields': ('..', '..', 'fields'), 'dimensions': ('..', '..', 'dimensions'),
-                         'global': ('boundary',)},
-            'expression': {'internal': ('internal',)}}
+                         'global': ('boundary',)}}
+        if expression:
+            processes['agents'][aid]['expression'] = EnzymeExpression(1e-4 * (1 + a % 3), 2.0)
+            topology['agents'][aid]['expression'] = {'internal': ('internal',)}
         internal = {k: v * (1 + 0.01 * a) for k, v in cfg['initial_state']['internal'].items()}
         agents[aid] = {'internal': internal, 'fluxes': {},
                        'boundary': {'location': locs[a], 'mmol_to_counts': mmol_to_counts(1339.0 + a),
@@ -129,6 +131,35 @@ def test_lattice_colony_through_the_loop_equals_reference_restatement():
     # the run exchanged with the field and diffused it
     ac = _to_host(gpu.state['fields']['ac_e'])
     assert ac.max() > 0 and np.count_nonzero(ac) > N
+
+
+@pytest.mark.parametrize('expression', [False, True])
+def test_columnar_agents_through_the_loop_equal_reference_restatement(expression):
+    """The same colony with its agents held in columns (lens_amd.agent_store): with
+    kinetics alone per agent the kinetics run is one scheduler entry, one pack
+    from the columns and one column apply (and the diffusion process's agent
+    leaves one column write); with a second process per agent the per-agent
+    path runs over row views.  Both equal the oracle loop bit for bit."""
+    from lens_amd.engine import Experiment
+    from lens_amd.invoke import BatchedInvoke
+    from oracle.experiment import OracleExperiment
+    if not torch.cuda.is_available():
+        pytest.skip('no GPU')
+    dev = torch.device('cuda', 0)
+    p, t, init = _colony(True, dev, expression)
+    gpu = Experiment({'processes': p, 'topology': t, 'initial_state': init, 'invoke': BatchedInvoke(dev),
+                      'agent_columns': ('agents',)})
+    p, t, init = _colony(False, dev, expression)
+    ref = OracleExperiment(p, t, init)
+    for interval in (1.0, 4.0, 0.5, 5.5):
+        gpu.update(interval)
+        ref.update(interval)
+        torch.cuda.synchronize()
+        assert gpu.local_time == ref.local_time
+        _compare(gpu.state['agents'], ref.state['agents'])
+        _compare(gpu.state['fields'], ref.state['fields'])
+    groups = [e for e in gpu._sched_cache[3] if type(e).__name__ == '_Group']
+    assert bool(groups) == (not expression)
 
 
 def test_diffusion_field_process_update_dict_vs_oracle():
