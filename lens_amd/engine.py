@@ -1029,9 +1029,16 @@ class Experiment:
         sched = None
         while time < interval:
             if seen != self._structure:
-                everything = self._walk(self.processes, ())
-                processes = [(p, s) for p, s in everything if not s.is_deriver()]
-                derivers = [(p, s) for p, s in everything if s.is_deriver()]
+                # the walk, kept while the process tree's structure stands (it moves with
+                # every _generate / _delete / _divide; the tree is not edited otherwise)
+                wc = self.__dict__.get('_walk_cache')
+                if wc is not None and wc[0] == self._structure and wc[1] is self.processes:
+                    processes, derivers = wc[2], wc[3]
+                else:
+                    everything = self._walk(self.processes, ())
+                    processes = [(p, s) for p, s in everything if not s.is_deriver()]
+                    derivers = [(p, s) for p, s in everything if s.is_deriver()]
+                    self._walk_cache = (self._structure, self.processes, processes, derivers)
                 if seen is None:
                     # columnar agents: runs of agent kinetics processes are scheduled as one
                     # entry each (one front, one invoke, one column apply), formed only here,
@@ -1039,7 +1046,7 @@ class Experiment:
                     # the next call while the process list and the store's structure stand
                     cache = self.__dict__.get('_sched_cache')
                     if (cache is not None and cache[0] == self._structure and cache[1] == self._version and
-                            cache[2] == processes):
+                            cache[2] is processes):
                         sched = cache[3]
                     else:
                         sched = self._schedule(processes, front)
@@ -1050,9 +1057,10 @@ class Experiment:
                     # split per member); no regrouping until the next call
                     front = _dissolve_groups(front)
                     sched = processes
+                if front:
+                    live = {p for p, _ in processes}
+                    front = {p: f for p, f in front.items() if p in live or p[0] == '__group__'}
                 seen = self._structure
-                live = {p for p, _ in processes}
-                front = {p: f for p, f in front.items() if p in live or type(p[0]) is str and p[0] == '__group__'}
             full_step = INFINITY
             invoke, states_of = self.invoke, self.process_states
             last = None
