@@ -223,14 +223,16 @@ int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
 
 /* vk_diffuse for one part of a row band's block (multi-GPU C4), so that the
  * halo exchange can run while the band computes what does not need it:
- *   VK_PART_INTERIOR  every pass of the block on the rows whose inputs at the
- *                     block's start are all owned (10 (p+1) rows in from each
- *                     side with halo rows, pass p);
- *   VK_PART_EDGES     the rest of every pass (the rows next to the halo);
+ *   VK_PART_INTERIOR  the first m = interior_passes passes of the block on the
+ *                     rows whose inputs at the block's start are all owned
+ *                     (10 (p+1) rows in from each side with halo rows, pass p);
+ *   VK_PART_EDGES     the rest of those m passes (the rows next to the halo),
+ *                     then the block's remaining passes whole;
  *   VK_PART_ALL       = vk_diffuse.
- * INTERIOR then EDGES (the halo in place before EDGES) equals vk_diffuse bit
- * for bit.  Only the 10-deep plan (vk_set_stencil_depth(10), a block of 10 k
- * substeps) of a band of more than 2 * sub_count owned rows splits; otherwise
+ * interior_passes <= 0 or > the block's passes means all of them.  INTERIOR
+ * then EDGES (the halo in place before EDGES) equals vk_diffuse bit for bit.
+ * Only the 10-deep plan (vk_set_stencil_depth(10), a block of 10 k substeps)
+ * of a band of more than 2 * sub_count owned rows splits; otherwise
  * VK_ERR_LIMIT (nothing launched).  Replaces the same reference call as
  * vk_diffuse (diffusion_field.py:385-407).                                 */
 enum { VK_PART_ALL = 0, VK_PART_INTERIOR = 1, VK_PART_EDGES = 2 };
@@ -238,7 +240,8 @@ int vk_diffuse_part(double *field, double *work0, double *work1, int32_t n_field
                     int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi,
                     int32_t lo_min, int32_t hi_max, int32_t edge_top, int32_t edge_bot,
                     int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
-                    const double *uniform, int32_t part, vk_stream_t stream);
+                    const double *uniform, int32_t part, int32_t interior_passes,
+                    vk_stream_t stream);
 
 /* As vk_diffuse for a call that ends at the last substep, except that the
  * last substep writes delta = new - field into `delta` (same layout; zero on

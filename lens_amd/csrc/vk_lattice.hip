@@ -164,12 +164,14 @@ __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ sr
 // cp (nullable): the agent coupling the pass carries (vk_diffuse_coupled).
 static void launch_pass(int k, hipStream_t s, const double *src, double *dst, const double *f0, int nf, int64_t fs,
                         int ny, int lo, int hi, int in_lo, int in_hi, int top, int bot, double coef, const double *mm,
-                        const VkPsCouple *cp) {
+                        const VkPsCouple *cp, bool strip = false) {
     if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11 && ((k & 1) || k == 10)) {
         // tolerance mode, pair-sum passes (the final pass writes the new field as is);
         // they are instantiated for k = 3, 5, 7, 9, 10, 11 (an even k < 10 takes the
-        // wave tiles below); variants 40-43: the stage-split 10-deep pass
-        if (g_stencil_kernel >= 40 &&
+        // wave tiles below); variant 40: the stage-split 10-deep pass -- not for the
+        // short edge strips of vk_diffuse_part (`strip`), whose passes are latency-bound
+        // and run faster as single-wave tiles of a few rows
+        if (g_stencil_kernel >= 40 && !strip &&
             vk_launch_sp(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp))
             return;
         vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
@@ -212,7 +214,7 @@ static std::vector<int> odd_plan(int sub_count) {
 static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
                         int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max, int32_t edge_top,
                         int32_t edge_bot, int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
-                        const double *uniform, int32_t part, vk_stream_t stream);
+                        const double *uniform, int32_t part, int32_t split_m, vk_stream_t stream);
 
 extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n_fields,
                           int64_t field_stride, int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min,
@@ -220,7 +222,7 @@ extern "C" int vk_diffuse(double *field, double *work0, double *work1, int32_t n
                           int32_t sub_count, int32_t n_sub, double coeff_dt, const double *uniform,
                           vk_stream_t stream) {
     return diffuse_impl(field, work0, work1, n_fields, field_stride, ny, row_lo, row_hi, lo_min, hi_max, edge_top,
-                        edge_bot, sub_begin, sub_count, n_sub, coeff_dt, uniform, VK_PART_ALL, stream);
+                        edge_bot, sub_begin, sub_count, n_sub, coeff_dt, uniform, VK_PART_ALL, 0, stream);
 }
 
 // Whether vk_diffuse_part can split this block: the 10-deep plan of a row band's
@@ -236,7 +238,7 @@ extern "C" int vk_diffuse_part(double *field, double *work0, double *work1, int3
                                int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max,
                                int32_t edge_top, int32_t edge_bot, int32_t sub_begin, int32_t sub_count,
                                int32_t n_sub, double coeff_dt, const double *uniform, int32_t part,
-                               vk_stream_t stream) {
+                               int32_t interior_passes, vk_stream_t stream) {
     if (part != VK_PART_ALL && part != VK_PART_INTERIOR && part != VK_PART_EDGES) {
         vk::set_error("vk_diffuse_part: part must be VK_PART_ALL / _INTERIOR / _EDGES");
         return VK_ERR_ARG;
@@ -246,13 +248,13 @@ extern "C" int vk_diffuse_part(double *field, double *work0, double *work1, int3
         return VK_ERR_LIMIT;
     }
     return diffuse_impl(field, work0, work1, n_fields, field_stride, ny, row_lo, row_hi, lo_min, hi_max, edge_top,
-                        edge_bot, sub_begin, sub_count, n_sub, coeff_dt, uniform, part, stream);
+                        edge_bot, sub_begin, sub_count, n_sub, coeff_dt, uniform, part, interior_passes, stream);
 }
 
 static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
                         int32_t ny, int32_t row_lo, int32_t row_hi, int32_t lo_min, int32_t hi_max, int32_t edge_top,
                         int32_t edge_bot, int32_t sub_begin, int32_t sub_count, int32_t n_sub, double coeff_dt,
-                        const double *uniform, int32_t part, vk_stream_t stream) {
+                        const double *uniform, int32_t part, int32_t split_m, vk_stream_t stream) {
     if (!field || n_fields < 0 || ny <= 0 || row_lo < lo_min || row_hi > hi_max || row_lo >= row_hi ||
         sub_begin < 0 || sub_count < 0 || sub_begin + sub_count > n_sub ||
         (int64_t)hi_max * ny > field_stride) {
@@ -313,10 +315,14 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
             // a side with halo rows -- and the edges are the rest of the pass's rows.
             // The interior passes read and write only interior rows of each buffer, the
             // edge passes read at most 20 rows into the interior of the pass before, which
-            // no later interior pass writes (it starts 10 rows deeper per pass), so all
-            // interior passes can run before any edge pass (while the halo arrives).
+            // no later interior pass writes (it starts 10 rows deeper per pass), so the
+            // interior of the first m passes can run before any edge pass (while the halo
+            // arrives).  Then (part EDGES) the edges of those m passes, and the remaining
+            // passes whole.
             const bool halo_top = !edge_top && row_lo > lo_min, halo_bot = !edge_bot && row_hi < hi_max;
+            const int m = (split_m <= 0 || split_m > P) ? P : split_m;
             for (int p = 0; p < P; ++p) {
+                if (part == VK_PART_INTERIOR && p >= m) break;
                 const int e = sub_begin + 10 * p + 9;
                 const int grow = last_in_call - e;
                 const int lo = max(lo_min, row_lo - grow);
@@ -326,7 +332,8 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
                 const int ihi = halo_bot ? row_hi - 10 * (p + 1) : hi;
                 int ranges[3][2];
                 int nr = 0;
-                if (part == VK_PART_ALL) {
+                const bool strip = part == VK_PART_EDGES && p < m;
+                if (part == VK_PART_ALL || (part == VK_PART_EDGES && p >= m)) {
                     ranges[nr][0] = lo, ranges[nr][1] = hi, ++nr;
                 } else if (part == VK_PART_INTERIOR) {
                     ranges[nr][0] = ilo, ranges[nr][1] = ihi, ++nr;
@@ -339,7 +346,7 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
                     if (olo >= ohi) continue;
                     const int in_lo = max(lo_min, olo - 10), in_hi = min(hi_max, ohi + 10);
                     launch_pass(10, s, p ? dsts[p - 1] : S, dsts[p], f0, n_fields, field_stride, ny, olo, ohi, in_lo,
-                                in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr);
+                                in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr, strip);
                     int rc = vk::launch_check("vk_diffuse kernel (depth 10)");
                     if (rc) return rc;
                 }

@@ -352,13 +352,20 @@ class Lattice:
         field for j == 0, else work[(j-1) & 1])."""
         return self.fields if j == 0 else (self.work0 if ((j - 1) & 1) == 0 else self.work1)
 
-    def _run_part(self, j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, part):
+    # passes of a band's first block whose interior runs while its halo exchange is in
+    # flight (vk_diffuse_part); the edges of those passes follow the halo, then the
+    # block's other passes whole.  Each interior-first pass costs a short, latency-bound
+    # edge launch later, so only as many as the transfer needs to hide
+    HALO_OVERLAP_PASSES = 3
+
+    def _run_part(self, j, cnt, n_sub, coeff_dt, mm, lo_min, hi_max, part, passes=None):
         """One part of a block (vk_diffuse_part); False if the block does not split."""
         rc = native._lib.vk_diffuse_part(
             native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1),
             len(self.molecules), self.field_stride, self.ny, self.row_lo, self.row_hi, lo_min,
             hi_max, int(self.edge_top), int(self.edge_bot), j, cnt, n_sub, coeff_dt,
-            native.ptr(mm), int(part), native.stream_handle())
+            native.ptr(mm), int(part), int(self.HALO_OVERLAP_PASSES if passes is None else passes),
+            native.stream_handle())
         if rc == native.VK_ERR_LIMIT:
             return False
         native.check(rc, 'vk_diffuse_part')

@@ -104,7 +104,7 @@ _SIGS = {
     'vk_diffuse': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                     _i32, _i32, _i32, _f64, _vp, _vp], ctypes.c_int),
     'vk_diffuse_part': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
-                         _i32, _i32, _i32, _f64, _vp, _i32, _vp], ctypes.c_int),
+                         _i32, _i32, _i32, _f64, _vp, _i32, _i32, _vp], ctypes.c_int),
     'vk_diffuse_delta': ([_vp, _vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32,
                           _i32, _i32, _i32, _f64, _vp, _vp], ctypes.c_int),
     'vk_diffuse_coupled': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _f64, _vp, _vp, _vp, _i32, _i64,

@@ -54,6 +54,8 @@ def whole_plane_ms(variant=20, depth=10, rows=34):
 
 
 XFER_US = float(os.environ.get('XFER_US', '0'))
+if os.environ.get('OVERLAP_PASSES'):       # passes whose interior runs beside the stand-in transfer
+    Lattice.HALO_OVERLAP_PASSES = int(os.environ['OVERLAP_PASSES'])
 _CYCLES_PER_US = None
 
 
@@ -137,6 +139,7 @@ def main():
                 band, ms, graph_ms = band_ms(world, halo, rows, variant, depth, overlap)
                 print(json.dumps({'world': world, 'band': list(band), 'halo': halo, 'rows': rows, 'variant': variant,
                                   'depth': depth, 'xfer_us': XFER_US, 'overlap': overlap,
+                                  'overlap_passes': Lattice.HALO_OVERLAP_PASSES,
                                   'ms_per_step': round(ms, 4), 'efficiency': round(whole / world / ms, 3),
                                   'graph_ms_per_step': round(graph_ms, 4),
                                   'graph_efficiency': round(whole / world / graph_ms, 3)}), flush=True)

@@ -145,13 +145,15 @@ def test_split_pass_full_c4_planes(dev):
     assert torch.equal(got.fields, ref.fields)
 
 
+@pytest.mark.parametrize('passes', [1, 3, 10])
 @pytest.mark.parametrize('mode,variant', [('fma', 20), ('fma', 40), ('exact', 20)])
 @pytest.mark.parametrize('world,halo', [(2, 100), (3, 100), (3, 50)])
-def test_band_interior_then_edges_equals_whole_plane(dev, mode, variant, world, halo):
-    """vk_diffuse_part: a band's first block as its interior passes (no halo
-    needed: they run while the halo exchange is in flight) and then its edge
-    passes equals the whole plane bit for bit -- both arithmetic modes, the
-    pair-sum and the stage-split kernels, one and two halo blocks per step."""
+def test_band_interior_then_edges_equals_whole_plane(dev, mode, variant, world, halo, passes):
+    """vk_diffuse_part: a band's first block as the interior of its first
+    `passes` passes (no halo needed: they run while the halo exchange is in
+    flight), then their edges and the other passes whole, equals the whole plane
+    bit for bit -- both arithmetic modes, the pair-sum and the stage-split
+    kernels, one and two halo blocks per step."""
     from lens_amd import native
     from lens_amd.distributed import row_bands
     from lens_amd.lattice import Lattice, n_substeps
@@ -185,9 +187,10 @@ def test_band_interior_then_edges_equals_whole_plane(dev, mode, variant, world, 
                 lo_min = lat.row_lo if lat.edge_top else 0
                 hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
                 coef = lat.diffusion * 0.01
-                if j == 0 and lat._run_part(j, cnt, n_sub, coef, mm, lo_min, hi_max, native.VK_PART_INTERIOR):
+                if j == 0 and lat._run_part(j, cnt, n_sub, coef, mm, lo_min, hi_max, native.VK_PART_INTERIOR,
+                                            passes):
                     split += 1
-                    assert lat._run_part(j, cnt, n_sub, coef, mm, lo_min, hi_max, native.VK_PART_EDGES)
+                    assert lat._run_part(j, cnt, n_sub, coef, mm, lo_min, hi_max, native.VK_PART_EDGES, passes)
                 else:
                     lat._run_block(j, cnt, n_sub, coef, mm, lo_min, hi_max)
             j += cnt
