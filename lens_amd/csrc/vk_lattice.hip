@@ -337,6 +337,13 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
                     ranges[nr][0] = lo, ranges[nr][1] = hi, ++nr;
                 } else if (part == VK_PART_INTERIOR) {
                     ranges[nr][0] = ilo, ranges[nr][1] = ihi, ++nr;
+                } else if (halo_top && halo_bot && ilo < ihi && g_stencil_mode == 1 && g_stencil_kernel >= 20) {
+                    // both strips as one launch (pair-sum pass with a row gap)
+                    const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
+                    vk_launch_ps10_strips(10, s, p ? dsts[p - 1] : S, dsts[p], f0, n_fields, field_stride, ny, lo, hi,
+                                          in_lo, in_hi, top_reflect, bot_reflect, coeff_dt, uniform, nullptr, ilo, ihi);
+                    int rc = vk::launch_check("vk_diffuse kernel (depth 10, edge strips)");
+                    if (rc) return rc;
                 } else {
                     if (halo_top) ranges[nr][0] = lo, ranges[nr][1] = ilo, ++nr;
                     if (halo_bot) ranges[nr][0] = ihi, ranges[nr][1] = hi, ++nr;

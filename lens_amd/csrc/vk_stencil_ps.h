@@ -361,7 +361,8 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
-                                                    const double *__restrict__ uniform, const VkPsCouple cp) {
+                                                    const double *__restrict__ uniform, const VkPsCouple cp,
+                                                    int gap_lo, int gap_hi, int chunks_a) {
     constexpr int KH = (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
     constexpr int W = 64 * C - 2 * KH;           // columns written per tile
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
@@ -370,8 +371,11 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     const int tx = wave % tiles_x;
     const int ty = (wave / tiles_x) % chunks_y;
     const int f = wave / (tiles_x * chunks_y);
-    const int c0 = out_lo + ty * rows_per_chunk;
-    const int c1 = min(c0 + rows_per_chunk, out_hi);
+    // rows [gap_lo, gap_hi) are not written (two strips in one launch, vk_diffuse_part):
+    // the first chunks_a chunks tile [out_lo, gap_lo), the rest [gap_hi, out_hi)
+    const bool second = ty >= chunks_a;
+    const int c0 = second ? gap_hi + (ty - chunks_a) * rows_per_chunk : out_lo + ty * rows_per_chunk;
+    const int c1 = min(c0 + rows_per_chunk, second ? out_hi : gap_lo);
     const int x0 = tx * W;
     // agent coupling: the gather reads the plane before this pass changes anything
     if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
@@ -384,12 +388,16 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
 
 template <int K, int PD, int C, int CP = 0>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
-            int in_lo, int in_hi, int top, int bot, double coef, const double *mm, const VkPsCouple *cp) {
+            int in_lo, int in_hi, int top, int bot, double coef, const double *mm, const VkPsCouple *cp,
+            int gap_lo = -1, int gap_hi = -1) {
     constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
     const int tiles_x = (ny + W - 1) / W;
-    const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
-    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
+    if (!(gap_lo >= out_lo && gap_lo <= gap_hi && gap_hi <= out_hi)) gap_lo = gap_hi = out_hi;
+    const int rows_a = gap_lo - out_lo, rows_b = out_hi - gap_hi;
+    const int rch = chunk_rows(rows_a + rows_b, tiles_x, nf);
+    const int chunks_a = (rows_a + rch - 1) / rch;
+    const int chunks_y = chunks_a + (rows_b + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
     const double c4 = 1.0 - 4.0 * coef;
     VkPsCouple none = {};
@@ -400,10 +408,12 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl);
+                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl,
+                           gap_lo, gap_hi, chunks_a);
     } else {
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl,
+                           gap_lo, gap_hi, chunks_a);
     }
 }
 

@@ -16,3 +16,12 @@ void vk_launch_ps10(VK_STENCIL_LAUNCH_ARGS) {
     else
         vk_ps::launch<10, 4, 2>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
 }
+
+// Both edge strips of a band's 10-deep pass in one launch (vk_diffuse_part): rows
+// [out_lo, out_hi) without [gap_lo, gap_hi).  The strips are a few dozen rows each,
+// so a pass is latency-bound, and one launch costs about what one strip did.
+void vk_launch_ps10_strips(VK_STENCIL_LAUNCH_ARGS, int gap_lo, int gap_hi) {
+    (void)f0; (void)k;
+    vk_ps::launch<10, 4, 2, 2>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp, gap_lo,
+                               gap_hi);
+}
