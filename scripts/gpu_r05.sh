@@ -6,6 +6,7 @@
 #   bench   the driver's default bench command (C4 on one GPU)
 #   gloo2   bench.py --gpus 2 without a launcher (it starts torch.distributed.run itself;
 #           gloo, both ranks on the one GPU)
+#   gloo4   the same with 4 ranks
 #   prof    rocprofv3 kernel trace + stats of the bench (no counters)
 #   pmc     the pass's counters (FETCH_SIZE, WRITE_SIZE, SQ), one rocprofv3 run per group
 #   sweep   scripts/stencil_sweep.py with $SWEEP_ARGS
@@ -32,6 +33,10 @@ for st in "$@"; do
       timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --no-cpu-baseline \
         > $O/bench_gloo2.log 2>&1 || { tail -30 $O/bench_gloo2.log; exit 4; }
       tail -1 $O/bench_gloo2.log | cut -c1-300 ;;
+    gloo4)
+      timeout -k 10 300 python bench.py --gpus 4 --dist-backend gloo --steps 3 --warmup 1 --no-cpu-baseline \
+        > $O/bench_gloo4.log 2>&1 || { tail -30 $O/bench_gloo4.log; exit 4; }
+      tail -1 $O/bench_gloo4.log | cut -c1-300 ;;
     prof)
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
         python3 bench.py --no-cpu-baseline > $O/bench_c4_rocprof.log 2>&1 || { tail -20 $O/bench_c4_rocprof.log; exit 5; }
