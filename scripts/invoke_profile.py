@@ -4,6 +4,8 @@ per-agent-step cost at several colony sizes, with and without Python's cyclic
 GC, and a cProfile of one size.
 
     python scripts/invoke_profile.py [--profile N] [n_agents ...]
+
+COLUMNS=1 holds the agents in columns (Experiment(config['agent_columns'])).
 """
 import cProfile
 import gc
@@ -28,7 +30,10 @@ def run(n, steps=3, gc_on=True, profile=False):
     from lens_amd.invoke import BatchedInvoke
     dev = torch.device('cuda', 0)
     p, t, init = build(n, dev)
-    exp = Experiment({'processes': p, 'topology': t, 'initial_state': init, 'invoke': BatchedInvoke(dev)})
+    cfg = {'processes': p, 'topology': t, 'initial_state': init, 'invoke': BatchedInvoke(dev)}
+    if os.environ.get('COLUMNS') == '1':
+        cfg['agent_columns'] = ('agents',)
+    exp = Experiment(cfg)
     exp.update(1.0)
     torch.cuda.synchronize()
     if not gc_on:
@@ -45,8 +50,9 @@ def run(n, steps=3, gc_on=True, profile=False):
             prof.disable()
         best = min(best, time.perf_counter() - t0)
     gc.enable()
-    print('agents %6d  gc %-3s  %.1f us per agent-step (min of %d calls of %d steps)'
-          % (n, 'on' if gc_on else 'off', best / (n * steps) * 1e6, 1 if prof else REPS, steps), flush=True)
+    print('agents %6d  gc %-3s  %.2f us per agent-step (min of %d calls of %d steps)%s'
+          % (n, 'on' if gc_on else 'off', best / (n * steps) * 1e6, 1 if prof else REPS, steps,
+             '  [columns]' if os.environ.get('COLUMNS') == '1' else ''), flush=True)
     if prof:
         s = io.StringIO()
         st = pstats.Stats(prof, stream=s)
