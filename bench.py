@@ -139,8 +139,6 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
         return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
     if mode == 'fma' and variant >= 20 and depth <= 11 and (depth % 2 == 1 or depth == 10):
         # k_diffuse_ps<K, PD, C, SC, CP> (vk_stencil_ps.h); SC = the rescaled form (coef not ~1/4)
-        if variant == 30 and depth in (9, 10):
-            return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 4>' % depth
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
             return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
         return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0>' % depth
@@ -150,7 +148,7 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
         return 'vk_nt::k_diffuse_wl<10, 3, false, true>'
     if depth == 10:    # the exact mode's 10-deep whole-step plan
         return 'vk_nt::k_diffuse_wl<10, 3, false>'
-    if variant in (6, 20, 30) and depth in (7, 9, 11):
+    if variant in (6, 20, 40) and depth in (7, 9, 11):
         return 'vk_nt::k_diffuse_wl<%d, 6, false>' % depth
     return 'k_diffuse_wl<%d, %d, false>' % (depth, 3 if variant == 2 else 6)
 
@@ -172,11 +170,11 @@ def parse(argv=None):
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 30, 40],
-                   help='tolerance mode: 20 = pair-sum passes (default on one GPU), 30 = pair-sum with the '
-                        'stage-0 ring held as 16-B vectors, 40 = the 10-deep pair-sum pass with its stages split '
+    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40],
+                   help='tolerance mode: 20 = pair-sum passes (default on one GPU), 40 = the 10-deep pair-sum '
+                        'pass with its stages split '
                         'over a workgroup\'s waves (default on row bands), 6 = the variant-6 FMA form; exact '
-                        'mode: 2 / 3 = wave tiles prefetching 3 / 6 rows, 6 (and 20, 30, 40) = 3 with streaming '
+                        'mode: 2 / 3 = wave tiles prefetching 3 / 6 rows, 6 (and 20, 40) = 3 with streaming '
                         'stores')
     p.add_argument('--stencil-depth', type=int, default=None,
                    help='substeps fused per HBM pass (odd, or 10: tolerance-mode whole steps as 10-deep passes); '

@@ -79,20 +79,20 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // Exact mode: 2 / 3 = wave tile lag-1 prefetching 3 / 6 rows, 6 = variant 3 with
 // streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
 // setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default),
-// 30 = its stage-0 ring held as 16-B vectors (a tie, kept as the no-drain alternate),
-// 6 = the variant-6 FMA form (4 FP64 ops per cell-substep instead of 3).
+// 40 = the stage-split 10-deep pass (vk_stencil_sp.h; row bands), 6 = the variant-6
+// FMA form (4 FP64 ops per cell-substep instead of 3).
 // Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
 // 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
 // 7 (streaming loads), 8-11 (four columns per lane, compact boundary body, split
 // stages, LDS-crossbar neighbours), 12-16 (prefetch ring, buffer stores, zigzag
-// chunks, 6-row prefetch at depth 10), 21-29 / 31 / 32 (pair-sum prefetch depths,
-// stagger, cache policies, one plane at a time, coupled-pass placements) -- none faster.
+// chunks, 6-row prefetch at depth 10), 21-32 (pair-sum prefetch depths, stagger,
+// cache policies, one plane at a time, coupled-pass placements, the stage-0 ring as
+// 16-B vectors: 30 tied variant 20 and was retired in round 5) -- none faster.
 static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 30 ||
-        variant == 40)
+    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40)
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
@@ -174,7 +174,8 @@ static void launch_pass(int k, hipStream_t s, const double *src, double *dst, co
         if (g_stencil_kernel >= 40 && !strip &&
             vk_launch_sp(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp))
             return;
-        vk_launch_ps_alt(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+        if (k == 10) vk_launch_ps10(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+        else vk_launch_ps(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
     } else if (k == 10 ||
                ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11))) {
         // variant 6 (streaming stores); k = 10 is the tolerance mode's 4-op FMA form

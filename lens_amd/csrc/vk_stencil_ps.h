@@ -1,5 +1,5 @@
-// Tolerance-mode fused stencil passes in pair-sum form (variant 20 and its vector-ring form 30; the
-// tolerance-mode default), instantiated by vk_stencil_ps*.hip.  diffusion_field.py:385-394 advances every cell by
+// Tolerance-mode fused stencil passes in pair-sum form (variant 20, the tolerance-mode
+// default), instantiated by vk_stencil_ps*.hip.  diffusion_field.py:385-394 advances every cell by
 // f += coef * (N + S + E + W - 4C); the exact mode reproduces scipy's
 // convolve rounding (vk_stencil_kernels.h).  The tolerance mode only has to
 // stay within 1e-13 of it, so it is free to regroup the four neighbours:
@@ -65,8 +65,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *row, in
 // right of the plane loads zeros (its columns are halo) and stores nothing.
 // CP: bit 0 = streaming (nt) loads (A/B only), bit 1 = plain (cached) stores -- the 10-deep
 // pass's choice when its planes fit the MALL (vk_stencil_ps10.hip); 0 = plain loads and
-// streaming stores, the default; bit 2 = the stage-0 ring holds each row as one 16-B vector
-// (variant 30, see PsState)
+// streaming stores, the default
 template <int C, bool CL, int CP = 0>
 __device__ __forceinline__ void ps_load(double (&out)[C], const double *__restrict__ row, const PsLane &L) {
     if constexpr (!CL) {
@@ -81,19 +80,6 @@ __device__ __forceinline__ void ps_load(double (&out)[C], const double *__restri
     } else {
 #pragma unroll
         for (int j = 0; j < C; ++j) out[j] = row[min(max(L.cA + j, 0), L.ny - 1)];
-    }
-}
-
-template <bool CL, int CP = 0>
-__device__ __forceinline__ dv2 ps_load_v(const double *__restrict__ row, const PsLane &L) {
-    if constexpr (!CL) {
-        const __amdgpu_buffer_rsrc_t rs = row_rsrc(row, L.ny);
-        return __builtin_bit_cast(dv2, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)L.loff, 0, (CP & 1) ? 2 : 0));
-    } else {
-        dv2 v;
-        v.x = row[min(max(L.cA, 0), L.ny - 1)];
-        v.y = row[min(max(L.cA + 1, 0), L.ny - 1)];
-        return v;
     }
 }
 
@@ -174,25 +160,12 @@ __device__ __forceinline__ void ps_stage(const double (&cn)[C], const double (&f
     if (GL) v[C - 1] = ps_sel(L.mgl, dpp_from_lane_above(v[0]), v[C - 1]);   // the ghost column, for the next stage
 }
 
-template <int K, int PD, int C, bool VR = false>
+template <int K, int PD, int C>
 struct PsState {
     static constexpr int NR = PD + 2;      // stage-0 ring: rows i-1, i and PD in flight
     double ring[NR][C];
     double Wa[K][C], Wb[K][C];             // stage q >= 1: centre / fresh rows, roles swap each iteration
     double Da[K][C], Db[K][C];             // d rows, double-buffered the same way
-};
-
-// VR (CP bit 2): the ring as 16-B vectors.  A 16-B buffer load lands in one aligned
-// 4-VGPR tuple; held as two separate doubles, the allocator split the ring rows across
-// tuples and closed every unrolled group with copies of rows still in flight behind a
-// drain of the load queue (s_waitcnt vmcnt(1) once per NR rows, hipcc -S).
-template <int K, int PD, int C>
-struct PsState<K, PD, C, true> {
-    static constexpr int NR = PD + 2;
-    static_assert(C == 2, "the vector ring holds a lane's two columns");
-    dv2 ring[NR];
-    double Wa[K][C], Wb[K][C];
-    double Da[K][C], Db[K][C];
 };
 
 struct PsArgs {
@@ -207,27 +180,18 @@ __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (in
 // Iteration i at ring phase U (row i sits in ring slot U): prefetch row i+PD,
 // run stages [0, ACT), store row i-K if STORE.
 template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U>
-__device__ __forceinline__ void ps_iter(PsState<K, PD, C, (CP & 4) != 0> &S, const PsArgs &A, const PsLane &L, int i) {
+__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i) {
     constexpr int NR = PD + 2;
     constexpr int P = U & 1;
     // keep iterations in program order: the scheduler would otherwise hoist the
     // unrolled group's row loads (and their registers) to its top
     __builtin_amdgcn_sched_barrier(0);
     double r0c[C], r0f[C];                 // stage 0's rows i-1 and i
-    if constexpr ((CP & 4) != 0) {
-        S.ring[(U + PD) % NR] = ps_load_v<GL && GR && EY, CP>(A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
-        const dv2 rc = S.ring[(U + NR - 1) % NR], rf = S.ring[U];
-        r0c[0] = rc.x;
-        r0c[1] = rc.y;
-        r0f[0] = rf.x;
-        r0f[1] = rf.y;
-    } else {
-        ps_load<C, GL && GR && EY, CP>(S.ring[(U + PD) % NR], A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
+    ps_load<C, GL && GR && EY, CP>(S.ring[(U + PD) % NR], A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
 #pragma unroll
-        for (int j = 0; j < C; ++j) {
-            r0c[j] = S.ring[(U + NR - 1) % NR][j];
-            r0f[j] = S.ring[U][j];
-        }
+    for (int j = 0; j < C; ++j) {
+        r0c[j] = S.ring[(U + NR - 1) % NR][j];
+        r0f[j] = S.ring[U][j];
     }
 #pragma unroll
     for (int q = 0; q < ACT; ++q) {
@@ -254,7 +218,7 @@ __device__ __forceinline__ void ps_iter(PsState<K, PD, C, (CP & 4) != 0> &S, con
 }
 
 template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int T>
-__device__ __forceinline__ void ps_fill(PsState<K, PD, C, (CP & 4) != 0> &S, const PsArgs &A, const PsLane &L, int is) {
+__device__ __forceinline__ void ps_fill(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int is) {
     if constexpr (T < 2 * K - 1) {
         constexpr int ACT = T / 2 + 1 < K ? T / 2 + 1 : K;
         ps_iter<K, PD, C, GL, GR, EY, SC, CP, ACT, false, T % (PD + 2)>(S, A, L, is + T);
@@ -266,7 +230,7 @@ __device__ __forceinline__ void ps_fill(PsState<K, PD, C, (CP & 4) != 0> &S, con
 // so that no state has to be merged across a skipped iteration: a flat list of
 // guarded iterations keeps both versions of every row live and costs ~60 VGPRs.
 template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u>
-__device__ __forceinline__ void ps_tail(PsState<K, PD, C, (CP & 4) != 0> &S, const PsArgs &A, const PsLane &L, int i, int n) {
+__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n) {
     constexpr int NR = PD + 2;
     if constexpr (u < NR - 1) {
         if (u < n) {
@@ -277,7 +241,7 @@ __device__ __forceinline__ void ps_tail(PsState<K, PD, C, (CP & 4) != 0> &S, con
 }
 
 template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int... Us>
-__device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsState<K, PD, C, (CP & 4) != 0> &S, const PsArgs &A,
+__device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsState<K, PD, C> &S, const PsArgs &A,
                                           const PsLane &L, int i, int i1) {
     constexpr int NR = PD + 2;
     constexpr int PH = (2 * K - 1) % NR;    // ring phase of the first steady iteration
@@ -288,7 +252,7 @@ __device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsS
 template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP>
 __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1) {
     constexpr int NR = PD + 2;
-    PsState<K, PD, C, (CP & 4) != 0> S;
+    PsState<K, PD, C> S;
 #pragma unroll
     for (int q = 0; q < K; ++q)
 #pragma unroll
@@ -296,17 +260,10 @@ __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0
     // iteration `is` = c0-K+1 is stage 0's d-only step (d of row c0-K for its
     // first useful row c0-K+1); it reads row is-1 from slot NR-1, row is from slot 0
     const int is = c0 - K + 1;
-    if constexpr ((CP & 4) != 0) {
-        S.ring[NR - 1] = ps_load_v<GL && GR && EY, CP>(A.s + clamp_row(is - 1, A.in_lo, A.in_hi) * L.ny64, L);
+    ps_load<C, GL && GR && EY, CP>(S.ring[NR - 1], A.s + clamp_row(is - 1, A.in_lo, A.in_hi) * L.ny64, L);
 #pragma unroll
-        for (int u = 0; u < PD; ++u)
-            S.ring[u] = ps_load_v<GL && GR && EY, CP>(A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
-    } else {
-        ps_load<C, GL && GR && EY, CP>(S.ring[NR - 1], A.s + clamp_row(is - 1, A.in_lo, A.in_hi) * L.ny64, L);
-#pragma unroll
-        for (int u = 0; u < PD; ++u)
-            ps_load<C, GL && GR && EY, CP>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
-    }
+    for (int u = 0; u < PD; ++u)
+        ps_load<C, GL && GR && EY, CP>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
     ps_fill<K, PD, C, GL, GR, EY, SC, CP, 0>(S, A, L, is);
     // steady: i = c0+K .. c1+K-1, one stored row each (rows c0 .. c1-1)
     ps_steady<K, PD, C, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);

@@ -48,8 +48,7 @@ def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
     """Select the fused-pass kernel and output rows per tile (0 = auto; -1 keeps);
     returns the previous variant.  Exact mode: 2 / 3 = lag-1 wave tiles with 3 / 6
     rows prefetched, 6 = 3 with streaming stores (the exact mode's default kernel).
-    Tolerance mode: 20 = pair-sum passes (the default), 30 = the same with the
-    stage-0 ring held as 16-B vectors, 40 = the pair-sum 10-deep pass with its
+    Tolerance mode: 20 = pair-sum passes (the default), 40 = the pair-sum 10-deep pass with its
     stages split over a workgroup's waves (the row-band choice; other depths run
     20), 6 = the 4-op FMA wave tiles.  Any other
     number (a retired variant) raises ValueError: the library would
@@ -62,7 +61,7 @@ def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
 
 
-STENCIL_VARIANTS = frozenset((2, 3, 6, 20, 30, 40))     # vk_set_stencil_kernel (vk_lattice.hip)
+STENCIL_VARIANTS = frozenset((2, 3, 6, 20, 40))     # vk_set_stencil_kernel (vk_lattice.hip)
 
 
 def stencil_mode(mode=None) -> str:

@@ -26,12 +26,13 @@ def test_settle_steps_disabled_and_capped():
 def test_stencil_kernel_names_follow_the_launch_rules():
     """The rocprof names the bench looks its pass up by: the 4096^2 x 2 pass (537 MB)
     streams its stores, a 10-deep pass of <= 192 MiB (C3's 1024^2 x 2) stores
-    through the caches (vk_stencil_ps10.hip), variant 30 is the vector ring."""
+    through the caches (vk_stencil_ps10.hip), variant 40 is the stage-split pass."""
     whole = 16 * 4096 * 4096 * 2
     assert bench.stencil_kernel_name(20, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(20, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
     assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
-    assert bench.stencil_kernel_name(30, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 4>'
+    assert bench.stencil_kernel_name(40, 10, 'fma', whole) == 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
+    assert bench.stencil_kernel_name(40, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
     assert bench.stencil_kernel_name(6, 10, 'exact') == 'vk_nt::k_diffuse_wl<10, 3, false>'
 

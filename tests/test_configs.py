@@ -8,7 +8,7 @@ and the SoA division oracle in ``oracle/colony.py``:
 * C2 (10k heterogeneous agents, held externals, 100 steps): every agent, every
   step vs the C oracle; a 304-agent sample's 100-step trajectory vs scipy
   odeint (``tests/golden/c2_odeint_traj.npz``, made by
-  ``tests/golden/make_c2_odeint.py``).
+  ``tests/golden/make_odeint_traj.py``).
 * C3 (100k agents, 1024^2, glucose + acetate): 5 Euler steps free-running,
   bit for bit; 5 DP45 steps, each from the GPU's step-start state.
 * C4 (1M agents, 4096^2 x 2): one full step, Euler bit for bit and DP45, plus

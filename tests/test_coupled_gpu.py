@@ -94,7 +94,7 @@ CASES = {
     # name: (nx, ny, agents, crowd, mode, depth, kernel, rows)
     'd10_ragged': (40, 300, 3000, 0, 'fma', 10, 20, 8),
     'd9_odd_plan': (40, 300, 3000, 0, 'fma', 9, 20, 8),
-    'd10_vector_ring': (40, 300, 3000, 0, 'fma', 10, 30, 8),
+    'd10_split_selected': (40, 300, 3000, 0, 'fma', 10, 40, 8),   # coupled passes run variant 20
     'd10_crowded': (33, 260, 2500, 90, 'fma', 10, 20, 12),
     'd10_narrow': (30, 50, 800, 40, 'fma', 10, 20, 0),
     'd7_tall_tiles': (70, 230, 4000, 0, 'fma', 7, 20, 64),
