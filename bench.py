@@ -222,14 +222,16 @@ def stencil_settings(args, world):
         # against 0.995 / 0.628 / 0.450 at depth 9, profiles/r03/r03x_rank_emulate.log)
         # (exact mode too since round 4: 1.830 / 1.850 / 1.827 against 1.873 / 1.867 / 1.908 ms
         # per C4 step at depth 9, profiles/r04/r04af/)
-        depth = 10 if args.workload == 'c4' else 9
+        # (C3 in the tolerance mode too, with the stage-split pass below)
+        depth = 10 if (args.workload == 'c4' or (args.workload == 'c3' and args.stencil_mode == 'fma')) else 9
     kernel = args.stencil_kernel
     if kernel is None:
-        # row bands (N > 1) in the tolerance mode: the stage-split 10-deep pass, whose
-        # taller chunks fill a band's passes better (a middle rank's step at N = 8 / 4 /
-        # 2: 0.335 / 0.499 / 0.792 against 0.372 / 0.544 / 0.884 ms with variant 20,
-        # profiles/r05/r05fg/); the whole plane keeps variant 20
-        kernel = 40 if (world > 1 and args.stencil_mode == 'fma' and depth == 10) else 20
+        # row bands (N > 1) and C3 in the tolerance mode: the stage-split 10-deep pass, whose
+        # chunks fill whole rounds of resident workgroups (vk_sp::round_rows; a middle rank's
+        # step at N = 8 / 4 / 2: 0.333 / 0.498 / 0.803 against 0.372 / 0.544 / 0.884 ms with
+        # variant 20, profiles/r05/r05fg/, r05r/; C3 0.222 against 0.320 ms per step with the
+        # 9-deep variant-20 plan, r05q/); the whole C4 plane keeps variant 20 (a tie, r05r/)
+        kernel = 40 if ((world > 1 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
     rows = args.stencil_rows
     if rows is None:
         # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of

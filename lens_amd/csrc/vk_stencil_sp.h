@@ -273,12 +273,47 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
     sp_dispatch<K, PD, C, NW, SC, CP>(w, ey || gl || gr || (ny % C) != 0, A, L, X, c0, c1);
 }
 
+// Workgroups of the kernel resident on the device at once (occupancy x CUs; 5 x 256
+// on MI355X at 65 VGPRs), asked once per process.
+template <int K, int PD, int C, int NW, int CP>
+int resident_groups() {
+    static int cached = 0;
+    if (cached == 0) {
+        int dev = 0, cus = 0, per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_diffuse_sp<K, PD, C, NW, true, CP>, 64 * NW, 0) !=
+                hipSuccess)
+            return 1280;
+        cached = per_cu * cus > 0 ? per_cu * cus : 1280;
+    }
+    return cached;
+}
+
+// Auto chunk rows: whole rounds of resident workgroups.  One round holds
+// per_round = resident / (tile columns x planes) chunks; the pass takes k rounds,
+// k chosen so that chunks stay near 75 rows (taller chunks re-read less halo, but
+// one round of very tall chunks leaves each SIMD's waves exposed).  Measured
+// (profiles/r05/r05p-r05r, ms per 100 substeps): C3's 1024^2 x 2 at 16 rows
+// (one round) 0.222 ms per step against 0.286 / 0.258 at 8 / 20 rows and 0.320 for
+// the 9-deep variant-20 plan; a middle rank's band at N = 8 / 4 / 2 at 45 / 77 / 68
+// rows 0.333 / 0.498 / 0.803 ms against 0.339 / 0.511 / 0.803 with the fixed rows.
+inline int round_rows(int out_rows, int per_round) {
+    per_round = per_round > 0 ? per_round : 1;
+    const int rows1 = (out_rows + per_round - 1) / per_round;
+    int k = (int)(rows1 / 75.0 + 0.5);
+    k = k > 0 ? k : 1;
+    const int rows = (out_rows + per_round * k - 1) / (per_round * k);
+    return rows > 8 ? rows : 8;
+}
+
 template <int K, int PD, int C, int NW, int CP = 0>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
             int in_lo, int in_hi, int top, int bot, double coef, const double *mm, int rows) {
     constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
     const int tiles_x = (ny + W - 1) / W;
+    if (rows <= 0) rows = round_rows(out_hi - out_lo, resident_groups<K, PD, C, NW, CP>() / (tiles_x * nf));
     const int chunks_y = (out_hi - out_lo + rows - 1) / rows;
     const int groups = tiles_x * chunks_y * nf;
     const double c4 = 1.0 - 4.0 * coef;

@@ -222,12 +222,15 @@ def test_c4_full_step_vs_c_oracle(dev, integrator, sort_agents):
 
 
 class _bench_stencil:
-    """The fused-pass settings bench.py runs at C4 on one GPU (bench.stencil_settings
-    with the bench's default arguments), restored afterwards."""
+    """The fused-pass settings bench.py runs for a workload on one GPU
+    (bench.stencil_settings with the bench's default arguments), restored afterwards."""
+
+    def __init__(self, workload='c4'):
+        self.workload = workload
 
     def __enter__(self):
         from lens_amd.lattice import stencil_depth, stencil_kernel, stencil_mode
-        args = bench.parse(['--workload', 'c4'])
+        args = bench.parse(['--workload', self.workload])
         self.settings = bench.stencil_settings(args, 1)
         mode, depth, kernel, rows = self.settings
         self.prev = (stencil_mode(mode), stencil_depth(depth), stencil_kernel(kernel, rows))
@@ -296,6 +299,28 @@ def test_c3_euler_five_steps_free_running_bitwise(dev):
         assert np.array_equal(post.conc, ref.conc), step
         for f in range(len(fields)):
             assert np.array_equal(post.fields[f], fields[f]), (step, f)
+
+
+def test_c3_bench_configuration_steps_vs_c_oracle(dev):
+    """C3 as bench.py times it: tolerance mode, 10-deep stage-split passes
+    (variant 40) with chunk rows filling whole rounds of workgroups, DP45,
+    agents in bin order (the fused gather), graph replay.  Three steps, each against the C oracle from the GPU's
+    step-start state: agents within 1e-9, fields within 1e-13 of the plane's
+    largest value (the tolerance mode's bar)."""
+    with _bench_stencil('c3') as (mode, depth, kernel, rows):
+        assert (mode, depth, kernel, rows) == ('fma', 10, 40, 0)
+        col, lat, _ = bench.build_rank(_args('c3', 'dopri5', sort_agents=True), 0, 1, dev)
+        nd = col.table.n_dyn
+        replay = col.capture(1.0, 1)
+        for step in range(3):
+            pre = _pull(col, lat)
+            replay()
+            col.check_status()
+            torch.cuda.synchronize()
+            post = _pull(col, lat)
+            conc, flux, counts, h, nsteps = _oracle_kinetics(col.table, 'dopri5', pre)
+            _rel_close(post.conc[:nd], conc[:nd], 1e-9)
+            _check_lattice_step(col, lat, pre, post, 'dopri5', counts, field_tol=1e-13)
 
 
 def test_c3_dopri5_five_steps_vs_c_oracle(dev):

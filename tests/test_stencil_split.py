@@ -61,7 +61,7 @@ def _run(dev, variant, rows, f0, diffusion=5.0, steps=1, second=None):
 
 
 @pytest.mark.parametrize('variant', SPLIT)
-@pytest.mark.parametrize('rows', [8, 33, 128, 300])
+@pytest.mark.parametrize('rows', [0, 8, 33, 128, 300])    # 0: whole rounds of workgroups (auto)
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517), (260, 1296), (17, 23), (64, 64), (40, 700), (129, 233)])
 def test_split_pass_equals_pair_sum_bitwise(dev, variant, rows, shape):
     rng = np.random.default_rng(hash((variant, rows) + shape) % 2**32)
