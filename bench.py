@@ -231,7 +231,8 @@ def stencil_settings(args, world):
         # step at N = 8 / 4 / 2: 0.333 / 0.498 / 0.803 against 0.372 / 0.544 / 0.884 ms with
         # variant 20, profiles/r05/r05fg/, r05r/; C3 0.222 against 0.320 ms per step with the
         # 9-deep variant-20 plan, r05q/); the whole C4 plane keeps variant 20 (a tie, r05r/)
-        kernel = 40 if ((world > 1 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
+        # (N = 2 keeps variant 20 since the edge-first tile order: 0.746 against 0.762 ms, r05w/)
+        kernel = 40 if ((world > 2 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
     rows = args.stencil_rows
     if rows is None:
         # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of

@@ -319,15 +319,14 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
                                                     const double *__restrict__ uniform, const VkPsCouple cp,
-                                                    int gap_lo, int gap_hi, int chunks_a) {
+                                                    int gap_lo, int gap_hi, int chunks_a, int ea, int eb) {
     constexpr int KH = (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
     constexpr int W = 64 * C - 2 * KH;           // columns written per tile
     const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int lane = threadIdx.x & 63;
     if (wave >= tiles_x * chunks_y * n_fields) return;
-    const int tx = wave % tiles_x;
-    const int ty = (wave / tiles_x) % chunks_y;
-    const int f = wave / (tiles_x * chunks_y);
+    int tx, ty, f;
+    vk_tile_of(wave, tiles_x, chunks_y, n_fields, ea, eb, tx, ty, f);
     // rows [gap_lo, gap_hi) are not written (two strips in one launch, vk_diffuse_part):
     // the first chunks_a chunks tile [out_lo, gap_lo), the rest [gap_hi, out_hi)
     const bool second = ty >= chunks_a;
@@ -356,6 +355,8 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     const int chunks_a = (rows_a + rch - 1) / rch;
     const int chunks_y = chunks_a + (rows_b + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
+    int ea = 0, eb = 0;     // (two strips in one launch: only the side columns go first)
+    if (chunks_a == chunks_y) vk_edge_chunks(K, out_lo, out_hi, rch, chunks_y, top, bot, ea, eb);
     const double c4 = 1.0 - 4.0 * coef;
     VkPsCouple none = {};
     const VkPsCouple &cpl = cp ? *cp : none;
@@ -366,11 +367,11 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
         for (int k = 0; k < K; ++k) cK *= c4;
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
                            out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl,
-                           gap_lo, gap_hi, chunks_a);
+                           gap_lo, gap_hi, chunks_a, ea, eb);
     } else {
         hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl,
-                           gap_lo, gap_hi, chunks_a);
+                           gap_lo, gap_hi, chunks_a, ea, eb);
     }
 }
 

@@ -221,8 +221,8 @@ template <int K, int PD, int C, int NW, bool SC, int CP = 0>
 __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict__ src, double *dst,
                                                        int64_t field_stride, int ny, int out_lo, int out_hi, int in_lo,
                                                        int in_hi, int top_reflect, int bot_reflect, int rows_per_chunk,
-                                                       int tiles_x, int chunks_y, double coef, double c4, double cK,
-                                                       const double *__restrict__ uniform) {
+                                                       int tiles_x, int chunks_y, int nf, int ea, int eb, double coef,
+                                                       double c4, double cK, const double *__restrict__ uniform) {
     constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
     constexpr int SLOTS = 2;     // hand-off slots per boundary
@@ -230,9 +230,8 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
     const int wg = blockIdx.x;
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int lane = threadIdx.x & 63;
-    const int tx = wg % tiles_x;
-    const int ty = (wg / tiles_x) % chunks_y;
-    const int f = wg / (tiles_x * chunks_y);
+    int tx, ty, f;
+    vk_tile_of(wg, tiles_x, chunks_y, nf, ea, eb, tx, ty, f);   // edge tiles first (vk_stencil_kernels.h)
     if (uniform && uniform[2 * f] == uniform[2 * f + 1]) return;     // a uniform plane keeps its values
     const int c0 = out_lo + ty * rows_per_chunk;
     const int c1 = min(c0 + rows_per_chunk, out_hi);
@@ -316,15 +315,19 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     if (rows <= 0) rows = round_rows(out_hi - out_lo, resident_groups<K, PD, C, NW, CP>() / (tiles_x * nf));
     const int chunks_y = (out_hi - out_lo + rows - 1) / rows;
     const int groups = tiles_x * chunks_y * nf;
+    int ea = 0, eb = 0;
+    vk_edge_chunks(K, out_lo, out_hi, rows, chunks_y, top, bot, ea, eb);
     const double c4 = 1.0 - 4.0 * coef;
     if (fabs(c4) >= 1e-3) {
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
         hipLaunchKernelGGL((k_diffuse_sp<K, PD, C, NW, true, CP>), dim3(groups), dim3(64 * NW), 0, st, src, dst, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rows, tiles_x, chunks_y, coef / c4, c4, cK, mm);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rows, tiles_x, chunks_y, nf, ea, eb, coef / c4, c4, cK,
+                           mm);
     } else {
         hipLaunchKernelGGL((k_diffuse_sp<K, PD, C, NW, false, CP>), dim3(groups), dim3(64 * NW), 0, st, src, dst, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rows, tiles_x, chunks_y, coef, c4, 1.0, mm);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rows, tiles_x, chunks_y, nf, ea, eb, coef, c4, 1.0,
+                           mm);
     }
 }
 

@@ -15,12 +15,14 @@ static void launch_wl(hipStream_t st, const double *src, double *dst, const doub
     const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
     const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
     const int waves = tiles_x * chunks_y * nf;
+    int ea = 0, eb = 0;
+    vk_edge_chunks(K, out_lo, out_hi, rch, chunks_y, top, bot, ea, eb);
     if (f0)
         hipLaunchKernelGGL((k_diffuse_wl<K, PD, true>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm, c);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm, c, ea, eb);
     else
         hipLaunchKernelGGL((k_diffuse_wl<K, PD, false>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, f0, fs,
-                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm, c);
+                           ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, mm, c, ea, eb);
 }
 
 template <int PD>
