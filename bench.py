@@ -771,6 +771,10 @@ def main():
         integ_flops = attempts * col.engine.dopri5_flops_per_attempt() / args.steps  # per step, rank 0
         variant = col.engine.default_variant()
         kname_i = {0: 'k_dopri5_thread', 1: 'k_dopri5_wave', 2: 'vk_dopri5_spec', 3: 'vk_dopri5_wspec'}[variant]
+        # the kinetics launch also gathers the next step's local environment (Colony.fuse_gather)
+        gathered = lat is not None and col._gather_fused() and not getattr(col, 'fuse_coupling', False)
+        if gathered:
+            kname_i = 'vk_dopri5_spec_gather'
         integ = {'kernel': kname_i, 'avg_ms_per_step': kin_ms,
                  'dp45_attempts_per_agent_step': attempts / agent_steps,
                  # integrator steps (accepted + rejected) and RHS evaluations
@@ -786,6 +790,8 @@ def main():
             # the agent state is streamed once per step: at a few flops per byte
             # (small networks) the launch is HBM-bound, not FP64-bound
             bpa = col.engine.dopri5_bytes_per_agent_step()
+            if gathered:   # + per gathered field: its value at the agent's bin read, the external row written
+                bpa += 16 * int(col.map_gather_field.numel())
             gbps = (agent_steps / args.steps) * bpa / (kin_ms * 1e-3) / 1e9
             t_flop = integ_flops / (FP64_PEAK_TFLOPS * 1e12)
             t_byte = (agent_steps / args.steps) * bpa / (HBM_PEAK_GBPS * 1e9)
