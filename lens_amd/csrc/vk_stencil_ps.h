@@ -303,14 +303,21 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
     const bool gr = x0 - KH + 64 * C >= ny;
     const bool ey = (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
                     (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
-    // Two bodies: interior tiles, and one general edge body (every edge kind,
-    // clamped columns).  Separate left / right bodies (16-B accesses, one ghost
-    // fix each) took the kernel past 168 VGPRs (2 waves per SIMD); the unscaled
-    // form (coef ~ 1/4) runs the general body everywhere.
-    if (!SC || ey || gl || gr || (ny % C) != 0)
+    // Three bodies: interior tiles; side tiles (a plane side in reach, no reflected
+    // row: 16-B accesses, both ghost fixes -- a no-op on the side the tile does not
+    // touch; C4 1.361 -> 1.337 ms per step, profiles/r05/r05ac/); and one general edge
+    // body (every edge kind, clamped columns: reflected rows, planes one tile wide,
+    // odd widths).  167 VGPRs (3 waves per SIMD); separate left / right bodies, or a
+    // fourth body for reflected rows alone (171), take it to 2 waves per SIMD.  The
+    // unscaled form (coef ~ 1/4) runs the general body everywhere.
+    if (!SC || ey || (gl && gr) || (ny % C) != 0)
         ps_body<K, PD, C, true, true, true, SC, CP>(A, L, c0, c1);
-    else if constexpr (SC)
-        ps_body<K, PD, C, false, false, false, SC, CP>(A, L, c0, c1);
+    else if constexpr (SC) {
+        if (gl || gr)
+            ps_body<K, PD, C, true, true, false, SC, CP>(A, L, c0, c1);
+        else
+            ps_body<K, PD, C, false, false, false, SC, CP>(A, L, c0, c1);
+    }
 }
 
 template <int K, int PD, int C, bool SC, int CP = 0>
