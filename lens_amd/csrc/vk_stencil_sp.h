@@ -200,17 +200,23 @@ __device__ __forceinline__ void sp_body(const PsArgs &A, const PsLane &L, SpXfer
     for (int b = S + 1; b < NW; ++b) sp_sync();
 }
 
+// body: 0 interior, 1 side tile (a plane side in reach, no reflected row: 16-B
+// accesses and both ghost fixes, as vk_stencil_ps.h's side body), 2 general
 template <int K, int PD, int C, int NW, bool SC, int CP, int S = 0>
-__device__ __forceinline__ void sp_dispatch(int w, bool general, const PsArgs &A, const PsLane &L, SpXfer &X,
+__device__ __forceinline__ void sp_dispatch(int w, int body, const PsArgs &A, const PsLane &L, SpXfer &X,
                                             int c0, int c1) {
     if constexpr (S < NW) {
         if (w == S) {
-            if (general || !SC)
+            if (body == 2 || !SC)
                 sp_body<K, PD, C, NW, S, true, true, true, SC, CP>(A, L, X, c0, c1);
-            else if constexpr (SC)
-                sp_body<K, PD, C, NW, S, false, false, false, SC, CP>(A, L, X, c0, c1);
+            else if constexpr (SC) {
+                if (body == 1)
+                    sp_body<K, PD, C, NW, S, true, true, false, SC, CP>(A, L, X, c0, c1);
+                else
+                    sp_body<K, PD, C, NW, S, false, false, false, SC, CP>(A, L, X, c0, c1);
+            }
         } else {
-            sp_dispatch<K, PD, C, NW, SC, CP, S + 1>(w, general, A, L, X, c0, c1);
+            sp_dispatch<K, PD, C, NW, SC, CP, S + 1>(w, body, A, L, X, c0, c1);
         }
     }
 }
@@ -269,7 +275,8 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
     const bool gr = x0 - KH + 64 * C >= ny;
     const bool ey = (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
                     (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
-    sp_dispatch<K, PD, C, NW, SC, CP>(w, ey || gl || gr || (ny % C) != 0, A, L, X, c0, c1);
+    const int body = (ey || (gl && gr) || (ny % C) != 0) ? 2 : ((gl || gr) ? 1 : 0);
+    sp_dispatch<K, PD, C, NW, SC, CP>(w, body, A, L, X, c0, c1);
 }
 
 // Workgroups of the kernel resident on the device at once (occupancy x CUs; 5 x 256
