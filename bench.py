@@ -301,21 +301,49 @@ def build_rank(args, rank, world, dev):
     return col, lat, (params, conc, loc if nx else None)
 
 
-def time_stencil_pass(lat, depth, reps=20):
-    """Average duration of ONE fused pass of `depth` substeps (non-final: fields ->
-    work buffer, fields untouched), HIP events on the launch stream."""
+def pass_plan(n_sub, depth):
+    """Substeps of each fused pass of one whole step, as vk_diffuse plans it
+    (vk_lattice.hip odd_plan / the 10-deep block plan)."""
+    if depth == 10 and n_sub % 10 == 0:
+        return [10] * (n_sub // 10)
+    d = min(9 if depth == 10 else depth | 1, 15)
+    passes = (n_sub + d - 1) // d
+    if (passes & 1) != (n_sub & 1):
+        passes += 1
+    ks, j, left = [], 0, passes
+    while j < n_sub:
+        rem = n_sub - j
+        k = (rem + left - 1) // left
+        k += 1 - (k & 1)
+        k = min(k, d)
+        while k > 1 and rem - k < left - 1:
+            k -= 2
+        ks.append(k)
+        j += k
+        left -= 1
+    return ks
+
+
+def time_stencil_pass(lat, depth, reps=5):
+    """Average duration of one fused pass of `depth` substeps as the step runs it:
+    whole 100-substep steps of the planes through vk_diffuse (its block plan, the
+    passes rotating through the three buffers, the cone of a row band), HIP events
+    on the launch stream, divided by the passes per step.  The planes are restored
+    afterwards.  (A single pass repeated on the same buffers ran ~5 % faster than
+    the same kernel inside the step, rocprof: profiles/r05/r05ah/.)"""
     from lens_amd import native
     lo_min = lat.row_lo if lat.edge_top else 0
     hi_max = lat.row_hi if lat.edge_bot else lat.rows_local
     coeff = lat.diffusion * 0.01
+    n_passes = len(pass_plan(100, depth))
+    saved = lat.fields.clone()
 
     def one():
         native.check(native._lib.vk_diffuse(
             native.ptr(lat.fields), native.ptr(lat.work0), native.ptr(lat.work1), len(lat.molecules),
             lat.field_stride, lat.ny, lat.row_lo, lat.row_hi, lo_min, hi_max, int(lat.edge_top),
-            int(lat.edge_bot), 0, depth, 100, coeff, 0, native.stream_handle()), 'vk_diffuse')
-    for _ in range(3):
-        one()
+            int(lat.edge_bot), 0, 100, 100, coeff, 0, native.stream_handle()), 'vk_diffuse')
+    one()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
@@ -323,7 +351,8 @@ def time_stencil_pass(lat, depth, reps=20):
         one()
     e1.record()
     torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    lat.fields.copy_(saved)
+    return e0.elapsed_time(e1) / (reps * n_passes)
 
 
 def time_copy_floor(lat, reps=20):

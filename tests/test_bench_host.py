@@ -123,3 +123,15 @@ def test_stencil_settings_pick_the_split_pass_for_row_bands():
     assert bench.stencil_settings(bench.parse(['--workload', 'c3', '--stencil-mode', 'exact']), 1) == \
         ('exact', 9, 20, 0)
     assert bench.stencil_kernel_name(40, 10, 'fma') == 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
+
+
+def test_pass_plan_restates_the_library_planner():
+    """bench.pass_plan (the passes time_stencil_pass divides a step's time by)
+    follows vk_diffuse: 10-deep blocks for multiples of 10, else odd passes of at
+    most 9 (depth 10's fallback) or the odd depth, as many as the parity needs."""
+    assert bench.pass_plan(100, 10) == [10] * 10
+    for n_sub, depth in ((100, 9), (501, 9), (1001, 11), (37, 10), (100, 7), (3, 15)):
+        ks = bench.pass_plan(n_sub, depth)
+        d = min(9 if depth == 10 else depth | 1, 15)
+        assert sum(ks) == n_sub and all(k % 2 == 1 and k <= d for k in ks), (n_sub, depth, ks)
+        assert len(ks) % 2 == n_sub % 2
