@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 GPU session.  Each argument is a stage, run in order; the session stops at
+# A GPU session.  Each argument is a stage, run in order; the session stops at
 # the first failure, and every GPU step has its own time limit.
 #   tests   pytest -m gpu (every GPU test, one process)
 #   smoke   __graft_entry__.smoke()
@@ -8,12 +8,14 @@
 #           gloo, both ranks on the one GPU)
 #   gloo4   the same with 4 ranks
 #   prof    rocprofv3 kernel trace + stats of the bench (no counters)
-#   pmc     the pass's counters (FETCH_SIZE, WRITE_SIZE, SQ), one rocprofv3 run per group
+#   pmc     the pass's counters (FETCH_SIZE, WRITE_SIZE, SQ), one rocprofv3 run per group, on
+#           scripts/stencil_once.py (DEPTH / ROWS / MODE / VARIANT / REPS from the environment;
+#           the bench pass: DEPTH=10 ROWS=34 MODE=fma VARIANT=20)
 #   sweep   scripts/stencil_sweep.py with $SWEEP_ARGS
 #   cmd     $CMD under a 300 s limit (output in $O/cmd.log)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-O=gpurun_out/${TAG:-r05}
+O=gpurun_out/${TAG:-session}
 mkdir -p $O
 export TMPDIR=/tmp
 for st in "$@"; do
