@@ -377,10 +377,9 @@ class Colony:
             with torch.cuda.stream(side):
                 if 'kin' in timing:
                     timing['kin'][0].record()
-                self.kinetics(dt)
+                self.kinetics_and_gather(dt)             # + the pre-step field (one-step lag)
                 if 'kin' in timing:
                     timing['kin'][1].record()
-                self.gather_external()                   # pre-step field (one-step lag)
                 done = torch.cuda.Event()
                 done.record()
             lat.diffuse(dt, halo_exchange=halo_exchange, allreduce=allreduce,
@@ -594,8 +593,9 @@ class Colony:
         replayed). Replaying a captured graph leaves the host out of the loop.
         Only steps that take no host decision can be captured: no division (the
         host reads back the new agent count), no row band (its halo exchange
-        is a host-driven collective), no NonSpatialEnvironment and no
-        side-stream overlap. A single-GPU lattice step qualifies: the pass plan
+        is a host-driven collective), no NonSpatialEnvironment. A single-GPU
+        lattice step qualifies (with ``overlap_kinetics`` too: the side stream
+        forks from and joins the captured stream inside each step): the pass plan
         depends only on Δt, and the uniform-plane skip is read by the kernels
         from device memory. Capture records the launches without running them,
         so the colony state is unchanged until the first replay. The graph
@@ -615,11 +615,10 @@ class Colony:
         slow each other and each cross-stream dependency adds ~6 us, 1.518 against
         1.515 ms per step (profiles/r04/r04k)."""
         lat = self.lattice
-        if (self.cells is not None or self.environment == 'nonspatial' or self.overlap_kinetics or
+        if (self.cells is not None or self.environment == 'nonspatial' or
                 (lat is not None and (lat.pad_top or lat.pad_bot or not (lat.edge_top and lat.edge_bot)))):
-            raise ValueError('Colony.capture: division, row bands, NonSpatialEnvironment and side-stream overlap '
-                             'take host decisions per step and cannot be replayed from one graph (a row band: '
-                             'capture_banded)')
+            raise ValueError('Colony.capture: division, row bands and NonSpatialEnvironment take host decisions '
+                             'per step and cannot be replayed from one graph (a row band: capture_banded)')
         if steps < 1:
             raise ValueError('Colony.capture: steps >= 1')
         spl = int(steps_per_launch)

@@ -620,7 +620,9 @@ def test_banded_depth10_plan_equals_whole(dev, mode):
 
 def test_lattice_colony_side_stream_overlap_is_exact(dev):
     """Kinetics + gather on the side stream beside the diffusion passes gives
-    the same fields and agent state, bit for bit, as the one-stream order."""
+    the same fields and agent state, bit for bit, as the one-stream order --
+    stepped eagerly and replayed from a captured graph (the side stream forks
+    from and joins the captured stream inside every step)."""
     from lens_amd.colony import Colony
     from lens_amd.lattice import Lattice
     cfg = configs.glc_ac_config()
@@ -630,20 +632,24 @@ def test_lattice_colony_side_stream_overlap_is_exact(dev):
     loc = rng.uniform(0, float(nx), (2, n))
     params, conc = configs.heterogeneous_colony(t, cfg, n, seed=5)
     out = []
-    for overlap in (False, True):
+    for overlap, graph in ((False, False), (True, False), (True, True)):
         lat = Lattice(['glc__D_e', 'ac_e'], (nx, nx), (float(nx), float(nx)), 10.0, 5.0, device=dev,
                       initial={'glc__D_e': configs.gaussian_bump_field((nx, nx)), 'ac_e': np.zeros((nx, nx))})
         col = Colony(cfg, n, device=dev, integrator='dopri5', environment=lat, table=t, specialize=True)
         col.overlap_kinetics = overlap
         col.set_agents(params=params, conc=conc, location=loc)
         col.gather_external()
-        for _ in range(3):
-            col.step(1.0)
+        if graph:
+            col.capture(1.0, 3)()
+        else:
+            for _ in range(3):
+                col.step(1.0)
         torch.cuda.synchronize()
         out.append((lat.owned('glc__D_e').cpu().numpy(), lat.owned('ac_e').cpu().numpy(),
                     col.conc[:, :n].cpu().numpy(), col.counts[:, :n].cpu().numpy()))
-    for a, b in zip(*out):
-        assert np.array_equal(a, b)
+    for got in out[1:]:
+        for a, b in zip(out[0], got):
+            assert np.array_equal(a, b)
 
 
 def test_lattice_colony_step_vs_oracle(dev):
