@@ -235,11 +235,12 @@ def stencil_settings(args, world):
         kernel = 40 if ((world > 2 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
     rows = args.stencil_rows
     if rows is None:
-        # 34-row tiles on the whole 4096^2 plane: 9,196 waves, just under 3 rounds of
-        # 3 waves x 1,024 SIMDs (64 rows: 4,864 waves, 1.58 rounds, 2.5-3 % slower per 100
-        # substeps, profiles/r03/r03h_stencil_rows_sweep.log, r03k_sweep.log); else the
-        # auto rule (chunk_rows)
-        rows = 34 if (world == 1 and args.workload == 'c4') else 0
+        # 64-row tiles on the whole 4096^2 plane (64 chunks of each plane exactly): since the
+        # edge-first tile order and the side-tile body, 1.290-1.307 ms per C4 step against
+        # 1.311 at 32 rows, 1.321-1.345 at 34 (the choice while the last wave round held the
+        # edge tiles, profiles/r03/r03h_stencil_rows_sweep.log), 1.320-1.327 at 68 and
+        # 1.35-1.61 at 60 / 72-128 (profiles/r05/r05an-r05ap); else the auto rule (chunk_rows)
+        rows = 64 if (world == 1 and args.workload == 'c4') else 0
     return args.stencil_mode, depth, kernel, rows
 
 

@@ -247,7 +247,7 @@ class _bench_stencil:
 def test_c4_bench_configuration_full_step_vs_c_oracle(dev):
     """The exact configuration the headline bench times: bench.build_rank's C4
     colony (1M agents, 4096^2 x 2) with the agents in bin order, DP45, and the
-    bench's fused passes (tolerance mode, 10-deep passes, 34-row tiles, the
+    bench's fused passes (tolerance mode, 10-deep passes, 64-row tiles, the
     default pair-sum kernel), stepped by replaying a captured HIP graph as the
     bench does.  One full step against the C oracle from the same start:
     agents within 1e-9 (and the north-star 1e-6 of the same algorithm),
@@ -256,7 +256,7 @@ def test_c4_bench_configuration_full_step_vs_c_oracle(dev):
     tolerance mode's bar, tests/test_stencil_modes.py), and per-bin count
     conservation of the exchange."""
     with _bench_stencil() as (mode, depth, kernel, rows):
-        assert (mode, depth, rows) == ('fma', 10, 34) and kernel >= 20
+        assert (mode, depth, rows) == ('fma', 10, 64) and kernel >= 20
         args = _args('c4', 'dopri5', sort_agents=True)
         col, lat, _ = bench.build_rank(args, 0, 1, dev)
         assert bool((col.bin_lin[1:col.n] >= col.bin_lin[:col.n - 1]).all())
