@@ -1002,6 +1002,20 @@ static int launch_dopri5(const vk_table *t, int64_t n, int64_t ld, double dt, co
 // One vk_step_dopri5 (variant 2) that also gathers the next step's local
 // environment: after the integration, conc[map_row[i] * ld + a] := plane
 // map_field[i] of `fields` at bin_lin[a], as vk_gather right after the kinetics.
+// Threads per block of the agent-per-lane specialised kernels: 256, or 64 when
+// the colony is small (fewer than 4 blocks of 256 per CU), so that its waves
+// spread over every CU instead of 4 to a CU on a few CUs (C2: 157 waves).
+static unsigned spec_threads(int64_t n) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return n < (int64_t)256 * 4 * cus ? 64u : 256u;
+}
+
 extern "C" int vk_step_dopri5_gather(const vk_table *t, int64_t n, int64_t ld, double dt, const vk_ode_opts *o,
                                      const double *params, double *conc, const double *m2c, double *h_state,
                                      double *flux, int64_t *counts, int32_t *status, int32_t *nsteps,
@@ -1028,8 +1042,8 @@ extern "C" int vk_step_dopri5_gather(const vk_table *t, int64_t n, int64_t ld, d
     void *args[] = {&n, &ld, &dt, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c, &h_state,
                     &flux, &counts, &status, &nsteps, (void *)&fields, &field_stride, (void *)&bin_lin,
                     (void *)&map_field, (void *)&map_row, &nm};
-    const unsigned blocks = (unsigned)((n + 255) / 256);
-    return vk::hip_check(hipModuleLaunchKernel(t->spec_gather, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream,
+    const unsigned th = spec_threads(n), blocks = (unsigned)((n + th - 1) / th);
+    return vk::hip_check(hipModuleLaunchKernel(t->spec_gather, blocks, 1, 1, th, 1, 1, 0, (hipStream_t)stream,
                                                args, nullptr),
                          "hipModuleLaunchKernel(vk_dopri5_spec_gather)");
 }
@@ -1063,8 +1077,8 @@ extern "C" int vk_step_dopri5_multi(const vk_table *t, int64_t n, int64_t ld, do
     int max_steps = o->max_steps, k = n_steps;
     void *args[] = {&n, &ld, &dt, &k, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c,
                     &h_state, &flux, &step_flux, &counts, &step_counts, &status, &nsteps, &step_nsteps};
-    const unsigned blocks = (unsigned)((n + 255) / 256);
-    return vk::hip_check(hipModuleLaunchKernel(t->spec_multi, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream, args,
+    const unsigned th = spec_threads(n), blocks = (unsigned)((n + th - 1) / th);
+    return vk::hip_check(hipModuleLaunchKernel(t->spec_multi, blocks, 1, 1, th, 1, 1, 0, (hipStream_t)stream, args,
                                                nullptr),
                          "hipModuleLaunchKernel(vk_dopri5_spec_multi)");
 }
@@ -1092,8 +1106,8 @@ extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double d
         int max_steps = o->max_steps;
         void *args[] = {&n, &ld, &dt, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c,
                         &delta, &h_state, &flux, &counts, &status, &nsteps};
-        const unsigned blocks = (unsigned)((n + 255) / 256);
-        return vk::hip_check(hipModuleLaunchKernel(t->spec_dopri5, blocks, 1, 1, 256, 1, 1, 0, (hipStream_t)stream,
+        const unsigned th = spec_threads(n), blocks = (unsigned)((n + th - 1) / th);
+        return vk::hip_check(hipModuleLaunchKernel(t->spec_dopri5, blocks, 1, 1, th, 1, 1, 0, (hipStream_t)stream,
                                                    args, nullptr),
                              "hipModuleLaunchKernel(vk_dopri5_spec)");
     }
