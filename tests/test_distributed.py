@@ -1,4 +1,4 @@
-"""Multi-rank row-band decomposition on CPU (gloo, world sizes 2 and 3).
+"""Multi-rank row-band decomposition on CPU (gloo, world sizes 2, 3 and 8).
 
 The halo-exchange protocol, band geometry, buffer rotation and the uniform-
 field all-reduce of lens_amd.distributed / Lattice.diffuse run for real over
@@ -94,7 +94,7 @@ def _worker(rank, world, port, halo, f0, result_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,halo', [(2, 10), (3, 7), (2, 1)])
+@pytest.mark.parametrize('world,halo', [(2, 10), (3, 7), (2, 1), (8, 5)])
 def test_banded_diffusion_gloo_matches_oracle(world, halo):
     rng = np.random.default_rng(world * 10 + halo)
     nx, ny = 41, 23
