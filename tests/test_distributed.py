@@ -221,7 +221,7 @@ def _router_worker(rank, world, port, seed, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,seed', [(2, 1), (3, 2)])
+@pytest.mark.parametrize('world,seed', [(2, 1), (3, 2), (8, 3)])
 def test_agent_router_routes_and_orders(world, seed):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
