@@ -318,6 +318,26 @@ __device__ __forceinline__ void vk_tile_of(int wave, int tiles_x, int chunks_y, 
     f = wave / (tiles_x * chunks_y);
 }
 
+// XCD-aware block order (speed only: any bijection computes the same cells).
+// Blocks are dealt round-robin over the 8 XCDs, so blocks b and b + 8 share an
+// L2.  Within each window of 8 * M blocks, block b takes slot (b % 8) * M +
+// (b / 8) % M of the window: each XCD runs M consecutive blocks of the order
+// above, side-by-side tiles that share their halo columns through its L2.  The
+// pair-sum pass uses M = 4 (16 tiles): C4 reads 371 -> 355 MB per launch; M = 9
+// was slower, and the stage-split pass (one tile per block) gained nothing
+// (profiles/r05/r05xcd*).
+template <int M>
+__device__ __forceinline__ int vk_xcd_block(int b, int nb) {
+    if constexpr (M > 1) {
+        constexpr int S = 8 * M;
+        if (b < nb / S * S) {
+            const int i = b % S;
+            return b - i + (i & 7) * M + (i >> 3);
+        }
+    }
+    return b;
+}
+
 // Edge chunk rows of a pass (host): the leading / trailing chunks whose reflected
 // rows are in reach -- the kernel's `ey` rule -- for the edge-first order.
 static inline void vk_edge_chunks(int K, int out_lo, int out_hi, int rch, int chunks_y, int top, int bot, int &ea,

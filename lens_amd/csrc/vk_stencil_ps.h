@@ -329,7 +329,8 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
                                                     int gap_lo, int gap_hi, int chunks_a, int ea, int eb) {
     constexpr int KH = (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
     constexpr int W = 64 * C - 2 * KH;           // columns written per tile
-    const int wave = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+    const int blk = vk_xcd_block<4>((int)blockIdx.x, (int)gridDim.x);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(blk * (blockDim.x >> 6) + (threadIdx.x >> 6)));
     const int lane = threadIdx.x & 63;
     if (wave >= tiles_x * chunks_y * n_fields) return;
     int tx, ty, f;

@@ -1,11 +1,12 @@
 #!/bin/bash
-# A/B of two builds of the library (lens_amd/lib/ab_base.so, ab_new.so) on the C4
-# bench, interleaved rounds; the new build is left installed.  $EXTRA: bench args.
+# A/B of builds of the library (lens_amd/lib/ab_<arm>.so for each arm in $ARMS,
+# default "base new") on the C4 bench, interleaved rounds; the last arm is left
+# installed.  $EXTRA: bench args.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${TAG:-libab}; mkdir -p $O
 for r in 1 2 3; do
-  for arm in base new; do
+  for arm in ${ARMS:-base new}; do
     cp lens_amd/lib/ab_$arm.so lens_amd/lib/libvk_kinetics.so
     timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 $EXTRA > $O/${arm}_$r.json 2> $O/${arm}_$r.err \
       || { echo "arm $arm failed"; tail -5 $O/${arm}_$r.err; exit 1; }

@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${TAG:-libabsmall}; mkdir -p $O
 for r in 1 2 3; do
-  for arm in base new; do
+  for arm in ${ARMS:-base new}; do
     cp lens_amd/lib/ab_$arm.so lens_amd/lib/libvk_kinetics.so
     line="$arm round $r:"
     for w in c2 c3; do

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/${TAG:-libabsplit}; mkdir -p $O
 for r in 1 2; do
-  for arm in base new; do
+  for arm in ${ARMS:-base new}; do
     cp lens_amd/lib/ab_$arm.so lens_amd/lib/libvk_kinetics.so
     timeout -k 10 200 python bench.py --workload c3 --no-cpu-baseline --steps 40 > $O/c3_${arm}_$r.json 2> $O/c3_${arm}_$r.err \
       || { echo "arm $arm failed"; tail -5 $O/c3_${arm}_$r.err; exit 1; }
