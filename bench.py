@@ -231,8 +231,11 @@ def stencil_settings(args, world):
         # step at N = 8 / 4 / 2: 0.333 / 0.498 / 0.803 against 0.372 / 0.544 / 0.884 ms with
         # variant 20, profiles/r05/r05fg/, r05r/; C3 0.222 against 0.320 ms per step with the
         # 9-deep variant-20 plan, r05q/); the whole C4 plane keeps variant 20 (a tie, r05r/)
-        # (N = 2 keeps variant 20 since the edge-first tile order: 0.746 against 0.762 ms, r05w/)
-        kernel = 40 if ((world > 2 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
+        # (N = 2 keeps variant 20 since the edge-first tile order: 0.746 against 0.762 ms, r05w/;
+        # N = 4 too since the XCD-aware block order of the pair-sum pass: 0.436 / 0.434 / 0.433
+        # against 0.447 / 0.439 / 0.434 ms, r05bm/, r05bn/; N = 8 keeps variant 40: 0.295 / 0.297
+        # against 0.305 / 0.305)
+        kernel = 40 if ((world > 4 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
     rows = args.stencil_rows
     if rows is None:
         # 64-row tiles on the whole 4096^2 plane (64 chunks of each plane exactly): since the

@@ -105,17 +105,19 @@ def test_bench_script_with_wrong_world_size_fails_before_importing_lens_amd():
 
 
 def test_stencil_settings_pick_the_split_pass_for_row_bands():
-    """One GPU: the pair-sum pass (variant 20) on 64-row tiles; row bands at N > 2
+    """One GPU: the pair-sum pass (variant 20) on 64-row tiles; row bands at N > 4
     and C3: the stage-split 10-deep pass (variant 40) with auto chunk rows; an explicit
     --stencil-kernel wins; the exact mode never takes the split pass."""
     args = bench.parse([])
     assert bench.stencil_settings(args, 1) == ('fma', 10, 20, 64)
     args = bench.parse([])
     assert bench.stencil_settings(args, 8) == ('fma', 10, 40, 0)
-    assert bench.stencil_settings(args, 4) == ('fma', 10, 40, 0)
+    assert bench.stencil_settings(args, 4) == ('fma', 10, 20, 0)
     assert bench.stencil_settings(args, 2) == ('fma', 10, 20, 0)
     args = bench.parse(['--stencil-kernel', '20'])
-    assert bench.stencil_settings(args, 4) == ('fma', 10, 20, 0)
+    assert bench.stencil_settings(args, 8) == ('fma', 10, 20, 0)
+    args = bench.parse(['--stencil-kernel', '40'])
+    assert bench.stencil_settings(args, 4) == ('fma', 10, 40, 0)
     args = bench.parse(['--stencil-mode', 'exact'])
     assert bench.stencil_settings(args, 2)[2] == 20
     # C3 (1024^2) on one GPU: 10-deep split passes, auto rows; its exact mode keeps depth 9
