@@ -707,8 +707,12 @@ class Colony:
             lat.uniform_summary(None)                    # the probe; its all-reduce is eager
         # the first block's interior needs no halo: it is its own graph, replayed while
         # the first halo exchange is in flight; the block's edges follow the halo
+        # the overlap decision is taken once, here: g_blocks[0] holds only the edge
+        # strips when the interior is split off, so step() must not re-read
+        # self.overlap_halo / self._comm_stream (a later toggle would drop the interior)
+        comm = self._comm_stream if self.overlap_halo else None
         g_interior = None
-        if self.overlap_halo and self._comm_stream is not None:
+        if comm is not None:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 j0, c0 = blocks[0]
@@ -732,8 +736,8 @@ class Colony:
                 raise RuntimeError('Colony.capture_banded: the colony was re-laid out after capture; capture again')
             main = torch.cuda.current_stream(self.device)
             halo_done = None
-            if self.overlap_halo and self._comm_stream is not None:
-                halo_done = lat.exchange_first_halo(dt, halo_exchange, self._comm_stream)
+            if comm is not None:
+                halo_done = lat.exchange_first_halo(dt, halo_exchange, comm)
             g_kin.replay()
             if allreduce is not None:
                 allreduce(lat.uniform)

@@ -217,12 +217,25 @@ class DeriveGlobals(ProcessBase):
         from lens_amd.cells import CellModel
         p = self.parameters
         self.model = CellModel(width=p['width'], density=p['density'], avogadro=AVOGADRO)
+        self._models = {(p['width'], p['density']): self.model}
 
     def is_deriver(self):
         return True
 
-    def _derived(self, mass):
-        volume, m2c, length, area = self.model.derive(mass)
+    def _model(self, width, density):
+        # derive_globals.py:133-135 reads width and density from the store on every
+        # call: one CellModel per (width, density) pair seen
+        key = (width, density)
+        m = self._models.get(key)
+        if m is None:
+            from lens_amd.cells import CellModel
+            m = self._models[key] = CellModel(width=width, density=density, avogadro=AVOGADRO)
+        return m
+
+    def _derived(self, mass, width=None, density=None):
+        p = self.parameters
+        model = self._model(p['width'] if width is None else width, p['density'] if density is None else density)
+        volume, m2c, length, area = model.derive(mass)
         return {'volume': volume, 'mmol_to_counts': m2c, 'length': length, 'surface_area': area,
                 'periplasm_volume': volume * self.parameters['periplasm_volume_fraction']}
 
@@ -249,7 +262,8 @@ class DeriveGlobals(ProcessBase):
         return {'global': schema}
 
     def next_update(self, timestep, states):
-        return {'global': self._derived(states['global']['mass'])}
+        g = states['global']
+        return {'global': self._derived(g['mass'], g.get('width'), g.get('density'))}
 
 
 def growth_division_minimal(agent_id, growth_rate=0.000275, boundary_path=('boundary',)):

@@ -890,7 +890,6 @@ class Experiment:
                       rows=rows, table=t, pack=pack, m2c=normalize_path(tuple(gl)) + ('mmol_to_counts',),
                       loc=shape[3] + ('location',), dyn=dyn_cols, flux=flux_cols, fields=fields,
                       dims=first_plan[4]['dimensions'], exch=first_plan[3], version=self._version,
-                      params=np.stack([p.param_values for p in procs], axis=1),
                       timestep=procs[0].local_timestep())
 
     def _invoke_group(self, g, timestep):
@@ -904,7 +903,10 @@ class Experiment:
         if m is None or not m[rows].all():
             raise KeyError('mmol_to_counts')
         m2c = t.gather(g.m2c, rows)
-        return self.invoke.group_call(g.procs, timestep, conc, m2c, g.params)
+        # the parameters are re-read every call, as the per-agent path reads
+        # process.param_values: an in-place change between update() calls reaches both
+        params = np.stack([p.param_values for p in g.procs], axis=1)
+        return self.invoke.group_call(g.procs, timestep, conc, m2c, params)
 
     def _apply_group(self, g, flux, delta, counts):
         """A group's kinetics outputs as column writes -- each agent's

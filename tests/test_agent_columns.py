@@ -94,3 +94,30 @@ def test_columnar_loop_is_flat_in_the_colony_size():
             best = min(best, time.process_time() - t0)
         per.append(best / (2 * n))
     assert per[1] < 1.6 * per[0] + 2e-6, per
+
+
+def test_group_reads_parameters_changed_in_place():
+    """A cached scheduler group re-reads its members' param_values on every call,
+    as the per-agent path reads process.param_values: an in-place change between
+    update() calls reaches the columnar launch too."""
+    seen = []
+
+    class Recording(hab.StubInvoke):
+        def flush(self):
+            for _, procs, _, _, _, params in self._groups:
+                seen.append(params.copy())
+            super().flush()
+
+    p, t, init = hab.build(8)
+    from lens_amd.engine import Experiment
+    exp = Experiment({'processes': p, 'topology': t, 'initial_state': init, 'invoke': Recording(),
+                      'agent_columns': ('agents',)})
+    for m in list(exp.state['fields']):
+        exp.state['fields'][m] = hab.host_field()
+    exp.update(1.0)
+    assert seen, 'the batched path did not run'
+    proc = p['agents']['a00003']['kinetics']
+    proc.param_values[0] = 12345.0
+    seen.clear()
+    exp.update(1.0)
+    assert seen and any((s == 12345.0).any() for s in seen)

@@ -367,7 +367,7 @@ def test_banded_multirate_run_equals_single_rank(world, halo, integrator):
 GSTEPS = 6
 
 
-def _graph_worker(rank, world, port, halo, q):
+def _graph_worker(rank, world, port, halo, q, toggle=False):
     import torch.distributed as dist
     os.environ['MASTER_ADDR'] = '127.0.0.1'
     os.environ['MASTER_PORT'] = str(port)
@@ -384,6 +384,10 @@ def _graph_worker(rank, world, port, halo, q):
         eager.step(1.0, halo_exchange=ex_e, allreduce=ar)        # first use of every kernel
         graphed.step(1.0, halo_exchange=ex_g, allreduce=ar)
         step = graphed.capture_banded(1.0, ex_g, ar)
+        if toggle:
+            # the overlap decision is frozen at capture: turning it off afterwards
+            # must not drop the first block's interior
+            graphed.overlap_halo = False
         same = []
         for _ in range(GSTEPS):
             eager.step(1.0, halo_exchange=ex_e, allreduce=ar)
@@ -399,8 +403,8 @@ def _graph_worker(rank, world, port, halo, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('world,halo', [(2, 100), (3, 7)])
-def test_banded_step_graph_replay_equals_eager(world, halo):
+@pytest.mark.parametrize('world,halo,toggle', [(2, 100, False), (3, 7, False), (2, 100, True)])
+def test_banded_step_graph_replay_equals_eager(world, halo, toggle):
     """Colony.capture_banded: each rank's step replayed as [kinetics + gather +
     uniform probe] and one graph per halo block, with the halo exchanges and
     the uniform all-reduce issued eagerly between them, equals the eager
@@ -413,7 +417,7 @@ def test_banded_step_graph_replay_equals_eager(world, halo):
     q = ctx.Queue()
     port = _free_port()
     halo = min(halo, NX // world)
-    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, halo, q)) for r in range(world)]
+    procs = [ctx.Process(target=_graph_worker, args=(r, world, port, halo, q, toggle)) for r in range(world)]
     for p in procs:
         p.start()
     parts = sorted([q.get(timeout=150) for _ in range(world)], key=lambda x: x[0])

@@ -260,3 +260,19 @@ def test_regenerated_path_takes_its_new_schema():
     exp._generate(('cells',), ('a',), {'leaf': Leaf('set')}, {'leaf': {'x': ('x',)}}, {'x': {'v': 1.0}})
     exp.update(1.0)
     assert exp.state['cells']['a']['x']['v'] == 2.0          # set, not accumulate
+
+
+def test_derive_globals_reads_width_and_density_from_the_store():
+    """derive_globals.py:133-135 takes density and width from states['global'] on
+    every call, not from the process parameters: a store holding other values
+    derives with those (the same formulas as a CellModel built with them)."""
+    from lens_amd.cells import CellModel
+    from lens_amd.division import AVOGADRO, DeriveGlobals
+    dg = DeriveGlobals()
+    default = dg.next_update(1.0, {'global': {'mass': 1500.0, 'width': 1, 'density': 1100.0}})['global']
+    other = dg.next_update(1.0, {'global': {'mass': 1500.0, 'width': 0.8, 'density': 1000.0}})['global']
+    vol, m2c, length, area = CellModel(width=0.8, density=1000.0, avogadro=AVOGADRO).derive(1500.0)
+    assert (other['volume'], other['mmol_to_counts'], other['length'], other['surface_area']) == (vol, m2c, length, area)
+    assert other['length'] != default['length']
+    # a store without the two leaves falls back to the parameters
+    assert dg.next_update(1.0, {'global': {'mass': 1500.0}})['global'] == default
