@@ -320,6 +320,12 @@ int vk_set_stencil_mode(int32_t mode);
  * replayed HIP graph with it (torch refuses events in graphs on ROCm).     */
 int vk_timestamp(uint64_t *out, int32_t idx, vk_stream_t stream);
 
+/* dst[0:n) = src[0:n) as the box's fastest streaming copy (one 16-B element per
+ * thread, non-temporal stores): the HBM floor any stencil pass over the same
+ * planes has (bench.py copy_floor).  Not a reference interface.  n even, both
+ * buffers 16-B aligned.                                                     */
+int vk_copy_stream(const double *src, double *dst, int64_t n, vk_stream_t stream);
+
 /* Tick rate of vk_timestamp's clock in kHz (hipDeviceAttributeWallClockRate
  * of the current device); 0 on error.                                       */
 int64_t vk_wall_clock_khz(void);

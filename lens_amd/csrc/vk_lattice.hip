@@ -141,6 +141,29 @@ extern "C" int vk_timestamp(uint64_t *out, int32_t idx, vk_stream_t stream) {
     return vk::launch_check("k_timestamp");
 }
 
+// The box's streaming-copy floor for a pass's planes: one 16-B element per thread,
+// non-temporal store, one wave of workgroups over the whole buffer.  Of the copy
+// shapes measured (scripts/micro/copy_floor.hip, profiles/r03/copy_floor.log) this
+// one is fastest: 84.4 us for a 4096^2 x 2 FP64 pair, 6.36 TB/s; grid-stride copies
+// and torch's copy_ reach 5.5-6.1.
+typedef double vk_d2v __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_copy_stream(const vk_d2v *__restrict__ s, vk_d2v *__restrict__ d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) __builtin_nontemporal_store(s[i], d + i);
+}
+
+extern "C" int vk_copy_stream(const double *src, double *dst, int64_t n_doubles, vk_stream_t stream) {
+    if (!src || !dst || n_doubles < 0 || (n_doubles & 1) || (((uintptr_t)src | (uintptr_t)dst) & 15)) {
+        vk::set_error("vk_copy_stream: bad arguments (16-B aligned buffers of an even number of doubles)");
+        return VK_ERR_ARG;
+    }
+    const int64_t n = n_doubles / 2;
+    if (n == 0) return VK_OK;
+    hipLaunchKernelGGL(k_copy_stream, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const vk_d2v *)src, (vk_d2v *)dst, n);
+    return vk::launch_check("k_copy_stream");
+}
+
 extern "C" int64_t vk_wall_clock_khz(void) {
     int dev = 0, khz = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;

@@ -28,7 +28,7 @@ EXPORTS = (
     'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy', 'vk_table_specialize',
     'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_step_dopri5_multi', 'vk_step_dopri5_gather', 'vk_field_uniform',
     'vk_diffuse', 'vk_diffuse_part', 'vk_diffuse_delta', 'vk_diffuse_coupled', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_set_stencil_mode',
-    'vk_timestamp', 'vk_wall_clock_khz', 'vk_gather', 'vk_exchange_sorted',
+    'vk_timestamp', 'vk_wall_clock_khz', 'vk_copy_stream', 'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites', 'vk_cell_step', 'vk_divide_scratch_bytes', 'vk_divide_plan',
     'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations', 'vk_kremling_step',
     'vk_expression_step',
@@ -114,6 +114,7 @@ _SIGS = {
     'vk_set_stencil_mode': ([_i32], ctypes.c_int),
     'vk_timestamp': ([_vp, _i32, _vp], ctypes.c_int),
     'vk_wall_clock_khz': ([], ctypes.c_int64),
+    'vk_copy_stream': ([_vp, _vp, _i64, _vp], ctypes.c_int),
     'vk_gather': ([_vp, _i64, _vp, _i64, _vp, _vp, _i32, _vp, _i64, _vp], ctypes.c_int),
     'vk_exchange_sorted': ([_vp, _i64, _vp, _vp, _vp, _i32, _vp, _i64, _vp, _vp, _i32, _f64, _vp],
                            ctypes.c_int),
