@@ -134,18 +134,16 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse):
     the full template argument list, as rocprofv3 prints it.  ``pass_bytes``
     (source + destination rows of one pass): a 10-deep pass of at most 192 MiB
-    stores through the caches (vk_stencil_ps10.hip), CP = 2."""
-    if mode == 'fma' and variant == 40 and depth == 10:
-        return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-    if mode == 'fma' and variant >= 20 and depth <= 11 and (depth % 2 == 1 or depth == 10):
+    stores through the caches (vk_stencil_ps10.hip), CP = 2.  The tolerance mode
+    runs pair-sum passes at depths 3-11 (odd) and 10, whatever the variant but 40;
+    other depths, and the exact mode, run the wave tiles (vk_lattice.hip launch_pass)."""
+    if mode == 'fma' and depth <= 11 and (depth % 2 == 1 or depth == 10):
+        if variant == 40 and depth == 10:
+            return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
         # k_diffuse_ps<K, PD, C, SC, CP> (vk_stencil_ps.h); SC = the rescaled form (coef not ~1/4)
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
             return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
         return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0>' % depth
-    if mode == 'fma' and depth in (7, 9, 11):
-        return 'vk_nt::k_diffuse_wl<%d, 6, false, true>' % depth
-    if mode == 'fma' and depth == 10:
-        return 'vk_nt::k_diffuse_wl<10, 3, false, true>'
     if depth == 10:    # the exact mode's 10-deep whole-step plan
         return 'vk_nt::k_diffuse_wl<10, 3, false>'
     if variant in (6, 20, 40) and depth in (7, 9, 11):

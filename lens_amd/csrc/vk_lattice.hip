@@ -78,16 +78,18 @@ __global__ __launch_bounds__(ST_BX) void k_diffuse_substep(const double *__restr
 int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h chunk_rows); 0 = auto
 // Exact mode: 2 / 3 = wave tile lag-1 prefetching 3 / 6 rows, 6 = variant 3 with
 // streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
-// setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default),
-// 40 = the stage-split 10-deep pass (vk_stencil_sp.h; row bands), 6 = the variant-6
-// FMA form (4 FP64 ops per cell-substep instead of 3).
+// setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default; 2 /
+// 3 / 6 select it too), 40 = the stage-split 10-deep pass (vk_stencil_sp.h; row
+// bands).  Tolerance-mode depths without a pair-sum pass (even depths below 10, 13,
+// 15) run the exact wave tiles.
 // Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
 // 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
 // 7 (streaming loads), 8-11 (four columns per lane, compact boundary body, split
 // stages, LDS-crossbar neighbours), 12-16 (prefetch ring, buffer stores, zigzag
 // chunks, 6-row prefetch at depth 10), 21-32 (pair-sum prefetch depths, stagger,
 // cache policies, one plane at a time, coupled-pass placements, the stage-0 ring as
-// 16-B vectors: 30 tied variant 20 and was retired in round 5) -- none faster.
+// 16-B vectors: 30 tied variant 20 and was retired in round 5), the tolerance-mode
+// FMA form of the wave tiles (4 FP64 ops per cell-substep; round 6) -- none faster.
 static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
@@ -99,10 +101,9 @@ extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
 }
 
 // 0 = bit-exact with scipy.ndimage.convolve (the default), 1 = tolerance mode: the
-// variant-6 passes with FMA-contracted arithmetic on a rescaled field (4 FP64 ops
-// per cell-substep instead of 6, vk_stencil_kernels.h) and no base re-read in the
-// final pass; fields agree with the exact mode to ~1e-14 relative
-// (tests/test_stencil_modes.py)
+// pair-sum passes (3 FP64 ops per cell-substep instead of 6, vk_stencil_ps.h) and no
+// base re-read in the final pass; fields agree with the exact mode to ~1e-14
+// relative (tests/test_stencil_modes.py)
 int g_stencil_mode = 0;
 
 extern "C" int vk_set_stencil_mode(int32_t mode) {
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(256) void k_copy_rows(const double *__restrict__ sr
 static void launch_pass(int k, hipStream_t s, const double *src, double *dst, const double *f0, int nf, int64_t fs,
                         int ny, int lo, int hi, int in_lo, int in_hi, int top, int bot, double coef, const double *mm,
                         const VkPsCouple *cp, bool strip = false) {
-    if (g_stencil_mode == 1 && g_stencil_kernel >= 20 && k <= 11 && ((k & 1) || k == 10)) {
+    if (g_stencil_mode == 1 && k <= 11 && ((k & 1) || k == 10)) {
         // tolerance mode, pair-sum passes (the final pass writes the new field as is);
         // they are instantiated for k = 3, 5, 7, 9, 10, 11 (an even k < 10 takes the
         // wave tiles below); variant 40: the stage-split 10-deep pass -- not for the
@@ -199,9 +200,8 @@ static void launch_pass(int k, hipStream_t s, const double *src, double *dst, co
             return;
         if (k == 10) vk_launch_ps10(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
         else vk_launch_ps(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
-    } else if (k == 10 ||
-               ((g_stencil_kernel == 6 || g_stencil_kernel >= 20 || g_stencil_mode == 1) && (k == 7 || k == 9 || k == 11))) {
-        // variant 6 (streaming stores); k = 10 is the tolerance mode's 4-op FMA form
+    } else if (k == 10 || ((g_stencil_kernel == 6 || g_stencil_kernel >= 20) && (k == 7 || k == 9 || k == 11))) {
+        // the exact mode's variant 6 (streaming stores), and its 10-deep whole-step plan
         vk_launch_wl6nt(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
     } else {
         // other depths (and variants 2 / 3): the plain-store wave tiles; the final pass
@@ -361,7 +361,7 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
                     ranges[nr][0] = lo, ranges[nr][1] = hi, ++nr;
                 } else if (part == VK_PART_INTERIOR) {
                     ranges[nr][0] = ilo, ranges[nr][1] = ihi, ++nr;
-                } else if (halo_top && halo_bot && ilo < ihi && g_stencil_mode == 1 && g_stencil_kernel >= 20) {
+                } else if (halo_top && halo_bot && ilo < ihi && g_stencil_mode == 1) {
                     // both strips as one launch (pair-sum pass with a row gap)
                     const int in_lo = max(lo_min, lo - 10), in_hi = min(hi_max, hi + 10);
                     vk_launch_ps10_strips(10, s, p ? dsts[p - 1] : S, dsts[p], f0, n_fields, field_stride, ny, lo, hi,

@@ -97,12 +97,11 @@ __device__ __forceinline__ double2 wt_load(const double *__restrict__ p, int64_t
 // ---------------------------------------------------------------------------
 
 // PD = rows prefetched ahead in VGPRs (a multiple of 3: the slot roles rotate with period 3)
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, bool STEADY, int U>
+template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U>
 __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                         const double *__restrict__ s, double *d,
                                         const double *g, const WtLane &L, int i, int c0, int c1,
-                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
-                                        double c4) {
+                                        int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
     constexpr int R = U % 3;
     double2(&UP)[K] = R == 0 ? S0 : (R == 1 ? S1 : S2);
     double2(&CN)[K] = R == 0 ? S1 : (R == 1 ? S2 : S0);
@@ -113,7 +112,7 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     const int r_out = i - K;
     const bool row_ok = STEADY || (r_out >= c0 && r_out < c1);
     double2 base = make_double2(0.0, 0.0);
-    if (FINAL && !FAST) {   // base row r_out arrived 3 iterations ago; fetch row r_out+3 (clamped into the chunk)
+    if (FINAL) {   // base row r_out arrived 3 iterations ago; fetch row r_out+3 (clamped into the chunk)
         base = gp[R];
         if (L.wA || L.wB) gp[R] = wt_load<EDGE>(g, (int64_t)min(max(r_out + 3, c0), c1 - 1) * ny, L);
     }
@@ -133,31 +132,13 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
             leftB = L.lB ? cen.y : leftB;
             rightB = L.rB ? cen.y : rightB;
         }
-        double2 v;
-        if (FAST && SC) {
-            // scaled tolerance mode: stage q carries the field divided by c4^q
-            // (c4 = 1 - 4coef), so c4*c + coef*sum becomes t + (coef/c4)*sum -- 4 FP64
-            // ops per cell; the last stage multiplies c4^K back in.  Here coef holds
-            // coef/c4 and c4 holds c4^K (diffuse_wl_tile)
-            const double sA = (up.x + dn.x) + (leftA + rightA);
-            const double sB = (up.y + dn.y) + (leftB + rightB);
-            v = make_double2(fma(coef, sA, cen.x), fma(coef, sB, cen.y));
-            if (q + 1 == K) v = make_double2(c4 * v.x, c4 * v.y);
-        } else if (FAST) {
-            // tolerance mode: c + coef*(N+S+E+W-4c) = fma(coef, (N+S)+(E+W), (1-4coef)*c),
-            // 5 FP64 ops per cell instead of 6
-            const double sA = (up.x + dn.x) + (leftA + rightA);
-            const double sB = (up.y + dn.y) + (leftB + rightB);
-            v = make_double2(fma(coef, sA, c4 * cen.x), fma(coef, sB, c4 * cen.y));
-        } else {
-            const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
-            const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
-            v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
-        }
+        const double lapA = ((fma(-4.0, cen.x, up.x + leftA)) + rightA) + dn.x;
+        const double lapB = ((fma(-4.0, cen.y, up.y + leftB)) + rightB) + dn.y;
+        double2 v = make_double2(cen.x + coef * lapA, cen.y + coef * lapB);
         if (q + 1 < K) {
             FR[q + 1] = v;
         } else if (row_ok) {
-            if (FINAL && !FAST) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
+            if (FINAL) v = make_double2(base.x + (v.x - base.x), base.y + (v.y - base.y));
             double *o = d + (int64_t)r_out * ny + L.cA;
             if (!EDGE) {
                 if (L.wA) wl_store(o, v);
@@ -169,46 +150,45 @@ __device__ __forceinline__ void wl_iter(double2 (&S0)[K], double2 (&S1)[K], doub
     }
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, bool STEADY, int U0, int... Us>
+template <int K, int PD, bool EDGE, bool FINAL, bool STEADY, int U0, int... Us>
 __device__ __forceinline__ void wl_group(double2 (&S0)[K], double2 (&S1)[K], double2 (&S2)[K],
                                          double2 (&pf)[PD], double2 (&gp)[3], const double *__restrict__ s, double *d,
                                          const double *g, const WtLane &L, int i, int c0, int c1,
-                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
-                                         double c4) {
-    wl_iter<K, PD, EDGE, FINAL, FAST, SC, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi,
-                                                  top_reflect, bot_reflect, coef, c4);
+                                         int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef) {
+    wl_iter<K, PD, EDGE, FINAL, STEADY, U0>(S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi,
+                                                  top_reflect, bot_reflect, coef);
     if constexpr (sizeof...(Us) > 0)
-        wl_group<K, PD, EDGE, FINAL, FAST, SC, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo,
-                                                          in_hi, top_reflect, bot_reflect, coef, c4);
+        wl_group<K, PD, EDGE, FINAL, STEADY, Us...>(S0, S1, S2, pf, gp, s, d, g, L, i + 1, c0, c1, in_lo,
+                                                          in_hi, top_reflect, bot_reflect, coef);
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC, int... Us>
+template <int K, int PD, bool EDGE, bool FINAL, int... Us>
 __device__ __forceinline__ void diffuse_wl_loop(std::integer_sequence<int, Us...>, double2 (&S0)[K],
                                                 double2 (&S1)[K], double2 (&S2)[K], double2 (&pf)[PD], double2 (&gp)[3],
                                                 const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
-                                                double coef, double c4) {
+                                                double coef) {
     const int i0 = c0 - K + 2, i1 = c1 + K;          // iterations [i0, i1)
     const int s_lo = c0 + K, s_hi = c1 + K - 1;      // every stage active for i in [s_lo, s_hi]
-#define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4
+#define WL_ARGS S0, S1, S2, pf, gp, s, d, g, L, i, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef
     constexpr int NU = PD;                           // iterations per unrolled group
     int i = i0;
-    for (; i + NU <= i1 && i < s_lo; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, false, Us...>(WL_ARGS);   // fill
-    for (; i + NU - 1 <= s_hi; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, true, Us...>(WL_ARGS);          // steady
-    for (; i + NU <= i1; i += NU) wl_group<K, PD, EDGE, FINAL, FAST, SC, false, Us...>(WL_ARGS);               // drain
+    for (; i + NU <= i1 && i < s_lo; i += NU) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);   // fill
+    for (; i + NU - 1 <= s_hi; i += NU) wl_group<K, PD, EDGE, FINAL, true, Us...>(WL_ARGS);          // steady
+    for (; i + NU <= i1; i += NU) wl_group<K, PD, EDGE, FINAL, false, Us...>(WL_ARGS);               // drain
     // tail: fewer than NU iterations, phases 0.. in order
-    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, FAST, SC, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1,
-                                                              in_lo, in_hi, top_reflect, bot_reflect, coef, c4)
+    ((i + Us < i1 ? wl_iter<K, PD, EDGE, FINAL, false, Us>(S0, S1, S2, pf, gp, s, d, g, L, i + Us, c0, c1,
+                                                              in_lo, in_hi, top_reflect, bot_reflect, coef)
                   : void()), ...);
 #undef WL_ARGS
 }
 
-template <int K, int PD, bool EDGE, bool FINAL, bool FAST, bool SC>
+template <int K, int PD, bool EDGE, bool FINAL>
 __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, double *d,
                                                 const double *g, const WtLane &L, int c0, int c1,
                                                 int in_lo, int in_hi, int top_reflect, int bot_reflect,
-                                                double coef, double c4) {
+                                                double coef) {
     double2 S0[K], S1[K], S2[K], pf[PD], gp[3];
 #pragma unroll
     for (int q = 0; q < K; ++q) S0[q] = S1[q] = S2[q] = make_double2(0.0, 0.0);
@@ -221,15 +201,15 @@ __device__ __forceinline__ void diffuse_wl_body(const double *__restrict__ s, do
     for (int u = 0; u < PD; ++u) pf[u] = wt_load<EDGE>(s, wl_row(L, i0 + u, in_lo, in_hi) * ny, L);
 #pragma unroll
     for (int u = 0; u < 3; ++u)   // FINAL: base rows of the first 3 output rows (i0 - K + u)
-        gp[u] = FINAL && !FAST && (L.wA || L.wB)
+        gp[u] = FINAL && (L.wA || L.wB)
                     ? wt_load<EDGE>(g, (int64_t)min(max(i0 - K + u, c0), c1 - 1) * ny, L)
                     : make_double2(0.0, 0.0);
-    diffuse_wl_loop<K, PD, EDGE, FINAL, FAST, SC>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L,
-                                              c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef, c4);
+    diffuse_wl_loop<K, PD, EDGE, FINAL>(std::make_integer_sequence<int, PD>(), S0, S1, S2, pf, gp, s, d, g, L,
+                                              c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
 // The stencil work of one wave: its tile of plane f, output rows [c0, c1)
-template <int K, int PD, bool FINAL, bool FAST>
+template <int K, int PD, bool FINAL>
 __device__ __forceinline__ void diffuse_wl_tile_body(const double *__restrict__ src, double *dst, const double *f0,
                                                      int64_t field_stride, int ny, int in_lo, int in_hi,
                                                      int top_reflect, int bot_reflect, double coef, int f, int x0,
@@ -251,30 +231,10 @@ __device__ __forceinline__ void diffuse_wl_tile_body(const double *__restrict__ 
     const bool edge = (x0 - KH <= 0) || (x0 - KH + WT_COLS >= ny) || (ny & 1) ||
                       (top_reflect >= c0 - 2 * K - 2 && top_reflect <= c1 + 2 * K) ||
                       (bot_reflect >= c0 - 2 * K - 2 && bot_reflect <= c1 + 2 * K);
-    const double c4 = 1.0 - 4.0 * coef;      // FAST only
-    if constexpr (FAST) {
-        // the scaled form while c4^-K stays far from overflow (|c4| >= 1e-3, i.e.
-        // coef not within 2.5e-4 of 1/4; coef = 0 gives the identity exactly)
-        if (fabs(c4) >= 1e-3) {
-            const double q = coef / c4;
-            double cK = 1.0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) cK *= c4;
-            if (edge)
-                diffuse_wl_body<K, PD, true, FINAL, FAST, true>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect,
-                                                                bot_reflect, q, cK);
-            else
-                diffuse_wl_body<K, PD, false, FINAL, FAST, true>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect,
-                                                                 bot_reflect, q, cK);
-            return;
-        }
-    }
     if (edge)
-        diffuse_wl_body<K, PD, true, FINAL, FAST, false>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect,
-                                                         coef, c4);
+        diffuse_wl_body<K, PD, true, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
     else
-        diffuse_wl_body<K, PD, false, FINAL, FAST, false>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect,
-                                                          bot_reflect, coef, c4);
+        diffuse_wl_body<K, PD, false, FINAL>(s, d, g, L, c0, c1, in_lo, in_hi, top_reflect, bot_reflect, coef);
 }
 
 // Dispatch order of a pass's tiles (wave index -> tile): the tiles that run the
@@ -352,9 +312,7 @@ static inline void vk_edge_chunks(int K, int out_lo, int out_hi, int rch, int ch
     while (ea + eb < chunks_y && ey(chunks_y - 1 - eb)) ++eb;
 }
 
-// FAST = tolerance mode (vk_set_stencil_mode(1)): FMA-contracted arithmetic and a
-// final pass without the base re-read; within ~1e-14 relative of the exact mode.
-template <int K, int PD, bool FINAL, bool FAST = false>
+template <int K, int PD, bool FINAL>
 __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, double *dst,
                                                 const double *f0, int64_t field_stride, int ny,
                                                 int out_lo, int out_hi, int in_lo, int in_hi, int top_reflect,
@@ -378,7 +336,7 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
     // changes anything; a uniform plane keeps its values and still takes the exchange
     if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
-        diffuse_wl_tile_body<K, PD, FINAL, FAST>(src, dst, f0, field_stride, ny, in_lo, in_hi, top_reflect,
+        diffuse_wl_tile_body<K, PD, FINAL>(src, dst, f0, field_stride, ny, in_lo, in_hi, top_reflect,
                                                  bot_reflect, coef, f, x0, c0, c1, lane);
     if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
@@ -398,9 +356,9 @@ __device__ __forceinline__ void diffuse_wl_tile(const double *__restrict__ src, 
 #ifndef VK_WL_WAVES_ATTR
 #define VK_WL_WAVES_ATTR
 #endif
-template <int K, int PD, bool FINAL, bool FAST = false>
+template <int K, int PD, bool FINAL>
 __global__ __launch_bounds__(256) VK_WL_WAVES_ATTR void k_diffuse_wl(VK_WL_PARAMS) {
-    diffuse_wl_tile<K, PD, FINAL, FAST>(VK_WL_ARGS);
+    diffuse_wl_tile<K, PD, FINAL>(VK_WL_ARGS);
 }
 
 // Rows per wave tile: g_stencil_rows, or (auto) by the height of the rows the

@@ -19,8 +19,6 @@ void vk_launch_wl6nt(VK_STENCIL_LAUNCH_ARGS) {
         vk_nt::launch<9, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
     else if (k == 11)
         vk_nt::launch<11, 6>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
-    else if (k == 10 && g_stencil_mode == 1)   // 3 rows prefetched keep it at 154 VGPRs (3 waves per SIMD)
-        vk_nt::launch_fast<10, 3>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
     else if (k == 10)   // the exact mode's 10-deep whole-step plan: 160 VGPRs (final pass: 178); PD is a
                         // multiple of 3 (the slot roles rotate with period 3)
         vk_nt::launch<10, 3>(st, src, dst, f0, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);

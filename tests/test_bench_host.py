@@ -35,6 +35,9 @@ def test_stencil_kernel_names_follow_the_launch_rules():
     assert bench.stencil_kernel_name(40, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
     assert bench.stencil_kernel_name(6, 10, 'exact') == 'vk_nt::k_diffuse_wl<10, 3, false>'
+    # the tolerance mode's wave-tile FMA form is retired: variant 6 selects the pair-sum pass
+    assert bench.stencil_kernel_name(6, 9, 'fma') == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
+    assert bench.stencil_kernel_name(20, 13, 'fma') == 'vk_nt::k_diffuse_wl<13, 6, false>'.replace('vk_nt::', '')
 
 
 class _FakeChild:

@@ -54,8 +54,8 @@ def _rel(got, ref):
     return float(np.abs(got - ref).max() / max(np.abs(ref).max(), 1e-300))
 
 
-@pytest.mark.parametrize("variant", [6, 20, 40])
-@pytest.mark.parametrize('depth', [3, 5, 7, 9, 10, 11])
+@pytest.mark.parametrize("variant", [20, 40])
+@pytest.mark.parametrize('depth', [3, 5, 7, 9, 10, 11, 13])   # 13: no pair-sum pass, the exact wave tiles
 def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
     from lens_amd.lattice import Lattice
     z = np.load(os.path.join(GOLDEN, 'stencil.npz'))
@@ -72,7 +72,7 @@ def test_fma_mode_vs_scipy_goldens(dev, depth, variant):
                 assert np.array_equal(lat.owned('b').cpu().numpy(), np.full((nx, ny), 2.5))
 
 
-@pytest.mark.parametrize("variant", [6, 20, 40])
+@pytest.mark.parametrize("variant", [20, 40])
 @pytest.mark.parametrize('depth,rows', [(9, 64), (7, 40), (11, 48), (9, 17), (10, 34), (10, 17), (10, 64), (5, 8), (9, 8)])
 @pytest.mark.parametrize('shape', [(700, 1000), (333, 517), (260, 1296)])
 def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape, variant):
