@@ -361,26 +361,31 @@ def time_stencil_pass(lat, depth, reps=5):
 
 def time_copy_floor(lat, reps=20):
     """Average duration of the box's fastest streaming copy of the planes a pass
-    streams (fields -> work0: one 8-B read + one 8-B write per cell, the
-    algorithmic bytes of one fused pass): vk_copy_stream, one 16-B element per
-    thread with a non-temporal store -- 84.4 us / 6.36 TB/s for the 4096^2 x 2
-    pair in scripts/micro/copy_floor.hip, where torch's copy_ (the round-1..5
-    floor) took ~99 us / 5.4 TB/s.  HIP events on the launch stream."""
+    streams (one 8-B read + one 8-B write per cell, the algorithmic bytes of one
+    fused pass): vk_copy_stream, one 16-B element per thread with a non-temporal
+    store -- 84.4 us / 6.36 TB/s for the 4096^2 x 2 pair in
+    scripts/micro/copy_floor.hip, where torch's copy_ (the round-1..5 floor) took
+    ~99 us / 5.4 TB/s.  HIP events on the launch stream.  The copies ping-pong
+    between the two work buffers (scratch between steps), so every copy reads
+    what the previous one streamed out past the 256 MiB Infinity Cache: one
+    source read twenty times over (fields -> work0) stays in that cache -- the
+    plane pair is 256 MiB -- and read at 7.4 TB/s (profiles/r06/r06c/), which is
+    no HBM floor."""
     from lens_amd import native
-    src = lat.fields.reshape(-1)
-    dst = lat.work0.reshape(-1)
-    n = src.numel() & ~1
+    bufs = (lat.work0.reshape(-1), lat.work1.reshape(-1))
+    n = bufs[0].numel() & ~1
 
-    def one():
+    def one(r):
+        src, dst = bufs[r & 1], bufs[1 - (r & 1)]
         native.check(native._lib.vk_copy_stream(native.ptr(src), native.ptr(dst), n, native.stream_handle()),
                      'vk_copy_stream')
-    for _ in range(3):
-        one()
+    for r in range(4):
+        one(r)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     e0.record()
-    for _ in range(reps):
-        one()
+    for r in range(reps):
+        one(r)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps, 16.0 * n

@@ -116,8 +116,26 @@ __device__ __forceinline__ void kremling_rhs(const Kp &p, const double (&s)[KS],
     da[2] = d[9];      // glc__D_e
 }
 
-__device__ __forceinline__ double step_factor(double en) {   // en ** -0.2
-    return exp2(-0.2 * log2(en));
+// en^-0.2 for the step-size factor (scipy RK45's error_norm ** (-1/5)) without
+// libm's exp2 / log2: a single-precision estimate from the hardware v_log_f32 /
+// v_exp_f32 (~1e-6 relative), then two Newton steps on en * y^5 = 1 in double
+// (quadratic: ~1e-11, then rounding).  en is clamped to [1e-30, 1e30] so the
+// float stays normal; outside that range the factor is capped anyway (at 10
+// for en < 1e-30, at 0.2 for en > 1e30, callers' fmin / fmax).  The same code in
+// every DP45 kernel (vk_kinetics.hip, the specialised templates, vk_kremling.hip)
+// keeps them bit-identical to one another.  exp2(log2()) kept its polynomial
+// constants in VGPRs across the attempt loop: the C5 wavefront kernel spilled
+// them and reloaded eight in series per attempt (round 6).
+__device__ __forceinline__ double step_factor(double en) {
+    const double e = fmin(fmax(en, 1e-30), 1e30);
+    double y = (double)__builtin_amdgcn_exp2f(-0.2f * __builtin_amdgcn_logf((float)e));
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double y2 = y * y;
+        const double r = fma(-e, y2 * y2 * y, 1.0);   // 1 - e y^5
+        y = fma(0.2 * y, r, y);
+    }
+    return y;
 }
 
 namespace dpk {

@@ -10,7 +10,7 @@ for r in $(seq 1 ${ROUNDS:-3}); do
   i=0
   for args in "$@"; do
     i=$((i+1))
-    timeout -k 10 200 python bench.py --no-cpu-baseline --steps 20 $args > $O/arm${i}_$r.json 2> $O/arm${i}_$r.err \
+    timeout -k 10 200 python bench.py --no-cpu-baseline --secondary-steps 0 --steps 20 $args > $O/arm${i}_$r.json 2> $O/arm${i}_$r.err \
       || { echo "arm $i ($args) failed"; tail -5 $O/arm${i}_$r.err; exit 1; }
     python -c "import json; d=json.loads(open('$O/arm${i}_$r.json').read().strip().splitlines()[-1]); r=d.get('roofline') or {}; print('arm $i [$args] round $r: %.4f ms/step  pass frac %s' % (d['ms_per_step'], r.get('frac')))"
   done
