@@ -201,7 +201,7 @@ def parse(argv=None):
                         'busy this long (power-management transient, profiles/r02g_eager_trace_gaps.log); '
                         'reported as untimed_settle_steps')
     p.add_argument('--no-cpu-baseline', action='store_true')
-    p.add_argument('--secondary-steps', type=int, default=5,
+    p.add_argument('--secondary-steps', type=int, default=10,
                    help='C4 on one GPU: timed steps of the bounded C5 and Kremling legs (0 = skip them)')
     p.add_argument('--cpu-seconds', type=float, default=12.0)
     args = p.parse_args(argv)
