@@ -57,17 +57,31 @@ __device__ __forceinline__ double kdiv(double a, double b) {
 }
 
 // x**e for the model's exponents: repeated products for a small integer e
-// (the reference's defaults n = 2, m = 1), pow otherwise
+// (the reference's defaults n = 2, m = 1), pow otherwise.  EI >= 0: the exponent
+// known at compile time (the kernel instantiated for it), so the products are
+// straight-line code inside the RHS instead of a loop per call -- the same
+// products in the same order, so the same bits.
+template <int EI>
 __device__ __forceinline__ double kpow(double x, double e, int ei) {
-    if (ei >= 0) {
+    if constexpr (EI >= 0) {
+        (void)e;
+        (void)ei;
         double r = 1.0;
-        for (int i = 0; i < ei; ++i) r *= x;
+#pragma unroll
+        for (int i = 0; i < EI; ++i) r *= x;
         return r;
+    } else {
+        if (ei >= 0) {
+            double r = 1.0;
+            for (int i = 0; i < ei; ++i) r *= x;
+            return r;
+        }
+        return pow(x, e);
     }
-    return pow(x, e);
 }
 
 // model(state, t) in the reference's operation order (Kremling2007_transport.py:220-351)
+template <int NI, int MI>
 __device__ __forceinline__ void kremling_rhs(const Kp &p, const double (&s)[KS], double (&d)[KS], double (&da)[KA]) {
     const double biomass = s[0], UHPT = s[1], LACZ = s[2], PTSG = s[3], G6P = s[4], PEP = s[5], PYR = s[6],
                  XP = s[7], GLC_e = s[8], G6P_e = s[9], LCTS_e = s[10];
@@ -97,7 +111,7 @@ __device__ __forceinline__ void kremling_rhs(const Kp &p, const double (&s)[KS],
     const double rgly = p.kgly * G6P;
     const double rpdh = p.kpdh * PYR;
     const double rpts = p.kpts * PEP * (p.x0 - XP) - p.km_pts * PYR * XP;
-    const double f = kpow(G6P, p.n, p.n_int) * kpow(PEP, p.m, p.m_int);
+    const double f = kpow<NI>(G6P, p.n, p.n_int) * kpow<MI>(PEP, p.m, p.m_int);
     const double rpyk = p.kpyk * PEP * f;
     const double mu = (g6p ? p.Y1_sim : p.Y3_sim) * uptake1 + p.Y2_sim * uptake2;
     d[0] = mu * biomass;
@@ -160,6 +174,9 @@ __device__ __forceinline__ int acc_of(int i) { return i == 11 || i == 12 ? 0 : i
 // device copy, not by value: as a by-value argument they are pinned in SGPRs
 // and ~1,400 SGPR spills to VGPR lanes follow; through the pointer the
 // compiler re-loads them (s_load) where registers run short.
+// NI / MI: the exponents n / m when the launch knows them as small integers (the
+// reference's n = 2, m = 1 have an instantiation of their own), -1 otherwise.
+template <int NI, int MI>
 __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k_kremling_dopri5(
                                                          const Kp *__restrict__ pp, int64_t n, int64_t ld, double grid_h, int n_grid,
                                                          double rtol, double atol, int max_steps,
@@ -178,7 +195,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
 #pragma unroll
     for (int j = 0; j < KA; ++j) ya[j] = 0.0;
     const double c0_glc = y[8], c0_g6p = y[9], c0_lcts = y[10];
-    kremling_rhs(p, y, k1, k1a);
+    kremling_rhs<NI, MI>(p, y, k1, k1a);
     int32_t st = 0;
     double h = h_state ? h_state[a] : 0.0;
     if (!(h > 0.0)) {   // scipy select_initial_step (order 4) over the first grid interval
@@ -196,7 +213,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
         h0 = fmin(h0, grid_h);
 #pragma unroll
         for (int i = 0; i < KS; ++i) yt[i] = fma(h0, k1[i], y[i]);
-        kremling_rhs(p, yt, k2, ka);
+        kremling_rhs<NI, MI>(p, yt, k2, ka);
         double d2 = 0.0;
 #pragma unroll
         for (int i = 0; i < KNY; ++i) {
@@ -227,29 +244,29 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
             for (int j = 0; j < KA; ++j) { s5[j] = dpk::b1 * k1a[j]; se[j] = dpk::e1 * k1a[j]; }
 #pragma unroll
             for (int i = 0; i < KS; ++i) yt[i] = fma(hs, dpk::a21 * k1[i], y[i]);
-            kremling_rhs(p, yt, k2, ka);                      // b2 = e2 = 0
+            kremling_rhs<NI, MI>(p, yt, k2, ka);                      // b2 = e2 = 0
 #pragma unroll
             for (int i = 0; i < KS; ++i) yt[i] = fma(hs, fma(dpk::a32, k2[i], dpk::a31 * k1[i]), y[i]);
-            kremling_rhs(p, yt, k3, ka);
+            kremling_rhs<NI, MI>(p, yt, k3, ka);
 #pragma unroll
             for (int j = 0; j < KA; ++j) { s5[j] = fma(dpk::b3, ka[j], s5[j]); se[j] = fma(dpk::e3, ka[j], se[j]); }
 #pragma unroll
             for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::a43, k3[i], fma(dpk::a42, k2[i], dpk::a41 * k1[i])), y[i]);
-            kremling_rhs(p, yt, k4, ka);
+            kremling_rhs<NI, MI>(p, yt, k4, ka);
 #pragma unroll
             for (int j = 0; j < KA; ++j) { s5[j] = fma(dpk::b4, ka[j], s5[j]); se[j] = fma(dpk::e4, ka[j], se[j]); }
 #pragma unroll
             for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::a54, k4[i], fma(dpk::a53, k3[i], fma(dpk::a52, k2[i], dpk::a51 * k1[i]))), y[i]);
-            kremling_rhs(p, yt, k5, ka);
+            kremling_rhs<NI, MI>(p, yt, k5, ka);
 #pragma unroll
             for (int j = 0; j < KA; ++j) { s5[j] = fma(dpk::b5, ka[j], s5[j]); se[j] = fma(dpk::e5, ka[j], se[j]); }
 #pragma unroll
             for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::a65, k5[i], fma(dpk::a64, k4[i], fma(dpk::a63, k3[i],
                             fma(dpk::a62, k2[i], dpk::a61 * k1[i])))), y[i]);
-            kremling_rhs(p, yt, k6, ka);
+            kremling_rhs<NI, MI>(p, yt, k6, ka);
 #pragma unroll
             for (int j = 0; j < KA; ++j) {
                 s5[j] = fma(dpk::b6, ka[j], s5[j]);
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void k
             for (int i = 0; i < KS; ++i)
                 yt[i] = fma(hs, fma(dpk::b6, k6[i], fma(dpk::b5, k5[i], fma(dpk::b4, k4[i],
                             fma(dpk::b3, k3[i], dpk::b1 * k1[i])))), y[i]);
-            kremling_rhs(p, yt, k7, ka);                      // FSAL: k7 is the next step's k1
+            kremling_rhs<NI, MI>(p, yt, k7, ka);                      // FSAL: k7 is the next step's k1
 #pragma unroll
             for (int j = 0; j < KA; ++j) se[j] = fma(dpk::e7, ka[j], se[j]);
             double en = 0.0;
@@ -426,7 +443,8 @@ extern "C" int vk_kremling_step(const vk_kremling_params *kp, int64_t n, int64_t
     const Kp *dp = nullptr;
     int rc = device_params(p, (hipStream_t)stream, &dp);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_kremling_dopri5, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, (hipStream_t)stream, dp,
+    auto kern = (p.n_int == 2 && p.m_int == 1) ? k_kremling_dopri5<2, 1> : k_kremling_dopri5<-1, -1>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, (hipStream_t)stream, dp,
                        n, ld, grid_h, n_grid, rtol, atol, max_steps, state, volume_fl, avogadro, h_state, flux,
                        counts, status, nsteps);
     return vk::launch_check("k_kremling_dopri5");
