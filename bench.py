@@ -955,7 +955,12 @@ def secondary_legs(args, dev):
         sub.workload, sub.steps, sub.warmup, sub.no_cpu_baseline = wl, args.secondary_steps, 3, True
         sub.stencil_mode, sub.stencil_depth, sub.stencil_kernel, sub.stencil_rows = 'fma', None, None, None
         sub.agents, sub.couple, sub.graph = None, False, 'auto'
-        o = run_kremling(sub, 0, 1, dev, None) if wl == 'kremling' else run(sub, 0, 1, dev, None)
+        try:
+            o = run_kremling(sub, 0, 1, dev, None) if wl == 'kremling' else run(sub, 0, 1, dev, None)
+        except Exception as e:          # a failed leg must not cost the headline its line
+            legs[wl] = {'error': '%s: %s' % (type(e).__name__, e), 'wall_s': time.perf_counter() - t0}
+            torch.cuda.empty_cache()
+            continue
         r = o['roofline']
         integ = o.get('integrator') or {}
         legs[wl] = {
