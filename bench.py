@@ -130,24 +130,16 @@ KREMLING_NY = 15
 SPLIT_STEPS = 6            # eager steps timed for the kinetics / diffusion split (the first is dropped)
 
 
-# variant -> (stash rows, XCD window, geometry) of k_diffuse_ps_vs (vk_stencil_ps10vs.hip)
-STASH_VARIANTS = {60: (16, 4, 0), 61: (16, 8, 0), 62: (17, 4, 0), 63: (16, 4, 1), 64: (16, 4, 2)}
-
-
-def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None, whole_chunks=True):
+def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
     """rocprof name of the non-final fused pass of `depth` substeps (vk_diffuse):
     the full template argument list, as rocprofv3 prints it.  ``pass_bytes``
     (source + destination rows of one pass): a 10-deep pass of at most 192 MiB
     stores through the caches (vk_stencil_ps10.hip), CP = 2.  The tolerance mode
     runs pair-sum passes at depths 3-11 (odd) and 10, whatever the variant but 40;
-    other depths, and the exact mode, run the wave tiles (vk_lattice.hip launch_pass).
-    Variants 60-62 (the 10-deep pass with the vertical stash) need whole 64-row chunks
-    (``whole_chunks``), else variant 20 runs."""
+    other depths, and the exact mode, run the wave tiles (vk_lattice.hip launch_pass)."""
     if mode == 'fma' and depth <= 11 and (depth % 2 == 1 or depth == 10):
         if variant == 40 and depth == 10:
             return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-        if variant in STASH_VARIANTS and depth == 10 and whole_chunks:
-            return 'vk_ps::k_diffuse_ps_vs<10, 4, 2, true, %s>' % ', '.join(map(str, STASH_VARIANTS[variant]))
         # k_diffuse_ps<K, PD, C, SC, CP> (vk_stencil_ps.h); SC = the rescaled form (coef not ~1/4)
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
             return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
@@ -176,7 +168,7 @@ def parse(argv=None):
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40, 60, 61, 62, 63, 64],
+    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40],
                    help='tolerance mode: 20 = pair-sum passes (default on one GPU), 40 = the 10-deep pair-sum '
                         'pass with its stages split '
                         'over a workgroup\'s waves (default on row bands), 6 = the variant-6 FMA form; exact '
@@ -870,9 +862,7 @@ def run(args, rank, world, dev, dist):
             bytes_per_launch = 16.0 * cells          # algorithmic: read + write each cell once
             achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
             traffic = valu = traffic_from = None
-            rows_out = lat.row_hi - lat.row_lo
-            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode, bytes_per_launch,
-                                        args.stencil_rows == 64 and rows_out % 64 == 0)
+            kname = stencil_kernel_name(args.stencil_kernel, depth, args.stencil_mode, bytes_per_launch)
             import glob
             for pmc in sorted(glob.glob(os.path.join(REPO, 'profiles', 'pmc_stencil*.json'))) if world == 1 else []:
                 with open(pmc) as f:

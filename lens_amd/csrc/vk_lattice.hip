@@ -94,7 +94,7 @@ static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40 || (variant >= 60 && variant <= 64))
+    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40)
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
@@ -197,10 +197,6 @@ static void launch_pass(int k, hipStream_t s, const double *src, double *dst, co
         // and run faster as single-wave tiles of a few rows
         if (g_stencil_kernel >= 40 && !strip &&
             vk_launch_sp(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp))
-            return;
-        if (k == 10 && g_stencil_kernel >= 60 && !strip &&
-            vk_launch_ps10_vs(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm,
-                              cp))
             return;
         if (k == 10) vk_launch_ps10(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
         else vk_launch_ps(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);

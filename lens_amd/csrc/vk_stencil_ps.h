@@ -54,10 +54,9 @@ struct PsLane {
 typedef int i4v __attribute__((ext_vector_type(4)));
 typedef double dv2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *row, int ny, bool live = true) {
-    // same descriptor word 3 as the variant-13 buffer stores of round 3; a row
-    // that is not live gets 0 records: its loads return zeros and touch no memory
-    return __builtin_amdgcn_make_buffer_rsrc((void *)row, 0, live ? ny * 8 : 0, 0x00020000);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *row, int ny) {
+    // same descriptor word 3 as the variant-13 buffer stores of round 3
+    return __builtin_amdgcn_make_buffer_rsrc((void *)row, 0, ny * 8, 0x00020000);
 }
 
 // CL = the general edge body (a row width the 16-B accesses cannot tile, a plane
@@ -68,10 +67,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const double *row, in
 // pass's choice when its planes fit the MALL (vk_stencil_ps10.hip); 0 = plain loads and
 // streaming stores, the default
 template <int C, bool CL, int CP = 0>
-__device__ __forceinline__ void ps_load(double (&out)[C], const double *__restrict__ row, const PsLane &L,
-                                        bool live = true) {
+__device__ __forceinline__ void ps_load(double (&out)[C], const double *__restrict__ row, const PsLane &L) {
     if constexpr (!CL) {
-        const __amdgpu_buffer_rsrc_t rs = row_rsrc(row, L.ny, live);
+        const __amdgpu_buffer_rsrc_t rs = row_rsrc(row, L.ny);
 #pragma unroll
         for (int j = 0; j < C; j += 2) {
             const i4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(L.loff + 8u * j), 0, (CP & 1) ? 2 : 0);
@@ -174,86 +172,26 @@ struct PsArgs {
     const double *s;
     double *d;
     int in_lo, in_hi, top, bot;
-    int row_end;            // the chunk's last input row + 1 (c1 + K): the ring's lookahead past it is not loaded
     double coef, c4, cK;
 };
 
 __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (int64_t)min(max(r, lo), hi - 1); }
 
-// Vertical stash (VS > 0, variants 60-62): a workgroup's 4 waves take 4 vertically
-// adjacent chunks of one column tile.  Chunk w's last 2K input rows are chunk w+1's
-// first 2K: the lower wave has them in registers during its fill, so it writes the
-// last VS of them to LDS, and the upper wave reads them from there ~60 iterations
-// later instead of from HBM (no cache bridges that distance: the rows are evicted
-// long before, profiles/r03/r03u/).  A flag per boundary, set after the rows (LDS
-// executes one wave's operations in order), orders the two waves.  The top wave
-// writes its rows to a trash row (no branch in the fill: a branch there costs 13
-// VGPRs), and the reads sit in an end segment unrolled at compile time (a branch per
-// iteration costs 33).
-typedef __attribute__((address_space(3))) i4v lds_i4v;
-typedef __attribute__((address_space(3))) volatile int lds_flag;
-struct PsStash {
-    lds_i4v *wr;        // the rows this wave hands to the wave above (the trash row for wave 0)
-    int wstride;        // i4v elements between written rows (0: the trash row)
-    lds_flag *wflag;
-    const lds_i4v *rd;  // the rows handed up by the wave below (the zero row if not linked)
-    int rstride;        // i4v elements between read rows (0: the zero row)
-    lds_flag *rflag;    // (a flag that is set if not linked)
-    bool linked;        // the chunk below is this group's: it hands its rows up
-    int lane;
-};
-
-__device__ __forceinline__ void stash_wait(const PsStash &X) {
-    while (*X.rflag == 0) __builtin_amdgcn_s_sleep(1);
-    // the rows were written before the flag: nothing may be read ahead of it
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-}
-
 // Iteration i at ring phase U (row i sits in ring slot U): prefetch row i+PD,
-// run stages [0, ACT), store row i-K if STORE.  FT >= 0: fill iteration FT (the
-// stash rows are written there).  SRC: where row i+PD comes from -- 0 HBM (not
-// loaded past the chunk's cone), 1 the stash (slot SLOT), 2 nowhere (past the cone).
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS, int ACT, bool STORE, int U,
-          int FT = -1, int SRC = 0, int SLOT = 0>
-__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, const PsStash &X,
-                                        int i) {
+// run stages [0, ACT), store row i-K if STORE.
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U>
+__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i) {
     constexpr int NR = PD + 2;
     constexpr int P = U & 1;
     // keep iterations in program order: the scheduler would otherwise hoist the
     // unrolled group's row loads (and their registers) to its top
     __builtin_amdgcn_sched_barrier(0);
     double r0c[C], r0f[C];                 // stage 0's rows i-1 and i
-    const int row = i + PD;
-    double(&slot)[C] = S.ring[(U + PD) % NR];
-    if constexpr (SRC == 0) {
-        // the last PD iterations' lookahead rows lie past the chunk's cone (4 of 88 rows read per
-        // 64-row chunk): not loaded
-        ps_load<C, GL && GR && EY, CP>(slot, A.s + clamp_row(row, A.in_lo, A.in_hi) * L.ny64, L, row < A.row_end);
-    } else if constexpr (SRC == 1) {
-        // a linked chunk reads the stash (its HBM load has 0 records: zeros, no traffic);
-        // any other reads the zero row and loads from HBM; the two are OR-ed
-        static_assert(C == 2, "the stash holds one 16-B element per lane and row");
-        double g[C];
-        ps_load<C, GL && GR && EY, CP>(g, A.s + clamp_row(row, A.in_lo, A.in_hi) * L.ny64, L, !X.linked);
-        if constexpr (SLOT == 0) stash_wait(X);
-        const i4v y = X.rd[SLOT * X.rstride + X.lane];
-        const i4v z = __builtin_bit_cast(i4v, make_double2(g[0], g[1])) | y;
-        const double2 v = __builtin_bit_cast(double2, z);
-        slot[0] = v.x;
-        slot[1] = v.y;
-    }
+    ps_load<C, GL && GR && EY, CP>(S.ring[(U + PD) % NR], A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
 #pragma unroll
     for (int j = 0; j < C; ++j) {
         r0c[j] = S.ring[(U + NR - 1) % NR][j];
         r0f[j] = S.ring[U][j];
-    }
-    if constexpr (VS > 0 && FT >= 0 && FT + 1 >= 2 * K - VS) {
-        // r0f is this chunk's input row FT + 1 (counted from c0 - K)
-        X.wr[(FT + 1 - (2 * K - VS)) * X.wstride + X.lane] = __builtin_bit_cast(i4v, make_double2(r0f[0], r0f[1]));
-        if constexpr (FT == 2 * K - 2) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            *X.wflag = 1;
-        }
     }
 #pragma unroll
     for (int q = 0; q < ACT; ++q) {
@@ -279,67 +217,40 @@ __device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, c
     }
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS, int T>
-__device__ __forceinline__ void ps_fill(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, const PsStash &X, int is) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int T>
+__device__ __forceinline__ void ps_fill(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int is) {
     if constexpr (T < 2 * K - 1) {
         constexpr int ACT = T / 2 + 1 < K ? T / 2 + 1 : K;
-        ps_iter<K, PD, C, GL, GR, EY, SC, CP, VS, ACT, false, T % (PD + 2), T>(S, A, L, X, is + T);
-        ps_fill<K, PD, C, GL, GR, EY, SC, CP, VS, T + 1>(S, A, L, X, is);
+        ps_iter<K, PD, C, GL, GR, EY, SC, CP, ACT, false, T % (PD + 2)>(S, A, L, is + T);
+        ps_fill<K, PD, C, GL, GR, EY, SC, CP, T + 1>(S, A, L, is);
     }
 }
 
 // The last (i1 - i) < NR iterations, nested (iteration u runs only if u-1 ran),
 // so that no state has to be merged across a skipped iteration: a flat list of
 // guarded iterations keeps both versions of every row live and costs ~60 VGPRs.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS, int PH, int u>
-__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, const PsStash &X, int i,
-                                        int n) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u>
+__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n) {
     constexpr int NR = PD + 2;
     if constexpr (u < NR - 1) {
         if (u < n) {
-            ps_iter<K, PD, C, GL, GR, EY, SC, CP, VS, K, true, (PH + u) % NR>(S, A, L, X, i + u);
-            ps_tail<K, PD, C, GL, GR, EY, SC, CP, VS, PH, u + 1>(S, A, L, X, i, n);
+            ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + u) % NR>(S, A, L, i + u);
+            ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, u + 1>(S, A, L, i, n);
         }
     }
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS, int... Us>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int... Us>
 __device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsState<K, PD, C> &S, const PsArgs &A,
-                                          const PsLane &L, const PsStash &X, int i, int i1) {
+                                          const PsLane &L, int i, int i1) {
     constexpr int NR = PD + 2;
     constexpr int PH = (2 * K - 1) % NR;    // ring phase of the first steady iteration
-    for (; i + NR <= i1; i += NR)
-        (ps_iter<K, PD, C, GL, GR, EY, SC, CP, VS, K, true, (PH + Us) % NR>(S, A, L, X, i + Us), ...);
-    ps_tail<K, PD, C, GL, GR, EY, SC, CP, VS, PH, 0>(S, A, L, X, i, i1 - i);
+    for (; i + NR <= i1; i += NR) (ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR>(S, A, L, i + Us), ...);
+    ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, 0>(S, A, L, i, i1 - i);
 }
 
-// A linked chunk (VS > 0) is VS_RCH rows tall: after NG groups of NR iterations from
-// HBM, its last iterations are unrolled with each row's source fixed at compile time.
-constexpr int VS_RCH = 64;
-
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS, int PH, int... Us>
-__device__ __forceinline__ void ps_group(std::integer_sequence<int, Us...>, PsState<K, PD, C> &S, const PsArgs &A,
-                                         const PsLane &L, const PsStash &X, int i) {
-    constexpr int NR = PD + 2;
-    (ps_iter<K, PD, C, GL, GR, EY, SC, CP, VS, K, true, (PH + Us) % NR>(S, A, L, X, i + Us), ...);
-}
-
-// iteration t (counted from c0 + K) of a linked chunk, t = T .. VS_RCH - 1
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS, int PH, int T>
-__device__ __forceinline__ void ps_end(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, const PsStash &X,
-                                       int i) {
-    if constexpr (T < VS_RCH) {
-        constexpr int NR = PD + 2;
-        constexpr int TG = VS_RCH - VS - PD;            // rows t + PD < VS_RCH + K - VS come from HBM
-        constexpr int SRC = T < TG ? 0 : (T < TG + VS ? 1 : 2);
-        ps_iter<K, PD, C, GL, GR, EY, SC, CP, VS, K, true, (PH + T) % NR, -1, SRC, SRC == 1 ? T - TG : 0>(S, A, L, X,
-                                                                                                          i);
-        ps_end<K, PD, C, GL, GR, EY, SC, CP, VS, PH, T + 1>(S, A, L, X, i + 1);
-    }
-}
-
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int VS>
-__device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, const PsStash &X, int c0, int c1) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP>
+__device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1) {
     constexpr int NR = PD + 2;
     PsState<K, PD, C> S;
 #pragma unroll
@@ -353,27 +264,16 @@ __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, const 
 #pragma unroll
     for (int u = 0; u < PD; ++u)
         ps_load<C, GL && GR && EY, CP>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
-    ps_fill<K, PD, C, GL, GR, EY, SC, CP, VS, 0>(S, A, L, X, is);
+    ps_fill<K, PD, C, GL, GR, EY, SC, CP, 0>(S, A, L, is);
     // steady: i = c0+K .. c1+K-1, one stored row each (rows c0 .. c1-1)
-    if constexpr (VS > 0) {
-        // every chunk is VS_RCH rows (the launcher's condition): the source of every row is
-        // known at compile time; no branch on `linked` (one after the fill costs ~100 VGPRs)
-        constexpr int PH = (2 * K - 1) % NR;
-        constexpr int NG = (VS_RCH - VS - PD) / NR;     // whole groups before the first stash row
-        int i = c0 + K;
-        for (int g = 0; g < NG; ++g, i += NR)
-            ps_group<K, PD, C, GL, GR, EY, SC, CP, VS, PH>(std::make_integer_sequence<int, NR>(), S, A, L, X, i);
-        ps_end<K, PD, C, GL, GR, EY, SC, CP, VS, PH, NG * NR>(S, A, L, X, i);
-    } else {
-        ps_steady<K, PD, C, GL, GR, EY, SC, CP, VS>(std::make_integer_sequence<int, NR>(), S, A, L, X, c0 + K, c1 + K);
-    }
+    ps_steady<K, PD, C, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);
 }
 
 // The stencil work of one wave: its tile of plane f, output rows [c0, c1)
-template <int K, int PD, int C, bool SC, int CP, int KH, int W, int VS = 0>
+template <int K, int PD, int C, bool SC, int CP, int KH, int W>
 __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double *dst, int64_t field_stride, int ny,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
-                                         double c4, double cK, int f, int x0, int c0, int c1, int lane, PsStash &X) {
+                                         double c4, double cK, int f, int x0, int c0, int c1, int lane) {
     PsLane L;
     L.ny = ny;
     L.ny64 = ny;
@@ -395,7 +295,6 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
     A.in_hi = in_hi;
     A.top = top_reflect;
     A.bot = bot_reflect;
-    A.row_end = c1 + K;
     A.coef = coef;
     A.c4 = c4;
     A.cK = cK;
@@ -412,12 +311,12 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
     // fourth body for reflected rows alone (171), take it to 2 waves per SIMD.  The
     // unscaled form (coef ~ 1/4) runs the general body everywhere.
     if (!SC || ey || (gl && gr) || (ny % C) != 0)
-        ps_body<K, PD, C, true, true, true, SC, CP, VS>(A, L, X, c0, c1);
+        ps_body<K, PD, C, true, true, true, SC, CP>(A, L, c0, c1);
     else if constexpr (SC) {
         if (gl || gr)
-            ps_body<K, PD, C, true, true, false, SC, CP, VS>(A, L, X, c0, c1);
+            ps_body<K, PD, C, true, true, false, SC, CP>(A, L, c0, c1);
         else
-            ps_body<K, PD, C, false, false, false, SC, CP, VS>(A, L, X, c0, c1);
+            ps_body<K, PD, C, false, false, false, SC, CP>(A, L, c0, c1);
     }
 }
 
@@ -445,74 +344,9 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     // agent coupling: the gather reads the plane before this pass changes anything
     if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     // a uniform plane keeps its values (zero delta); the exchange still applies
-    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1])) {
-        PsStash X = {};
+    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
         ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
-                                          c4, cK, f, x0, c0, c1, lane, X);
-    }
-    if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
-}
-
-// Variant 60: the pass with the vertical stash (PsStash above).  Block = group g of
-// 4 chunks (ty = 4g + w) of one column tile; groups in the edge-first, XCD-windowed
-// order of the wave tiles (a group is an edge group if any of its chunks is).
-// GEO (A/B of what the stash costs): 0 = the stash; 1 = the same groups, no row read
-// from the stash; 2 = variant 20's tile order (4 side-by-side tiles per block), no stash
-template <int K, int PD, int C, bool SC, int VS, int XM, int GEO = 0>
-__global__ __launch_bounds__(256) void k_diffuse_ps_vs(const double *__restrict__ src, double *dst,
-                                                       int64_t field_stride, int ny, int out_lo, int out_hi, int in_lo,
-                                                       int in_hi, int top_reflect, int bot_reflect, int rows_per_chunk,
-                                                       int tiles_x, int chunks_y, int groups_y, int n_fields,
-                                                       double coef, double c4, double cK,
-                                                       const double *__restrict__ uniform, const VkPsCouple cp, int ga,
-                                                       int gb) {
-    constexpr int KH = (K + C - 1) / C * C;
-    constexpr int W = 64 * C - 2 * KH;
-    // three boundaries' rows, the trash row (wave 0's writes), the zero row
-    __shared__ i4v stash[(3 * VS + 2) * 64];
-    __shared__ int flags[5];
-    const int blk = vk_xcd_block<XM>((int)blockIdx.x, (int)gridDim.x);
-    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = threadIdx.x & 63;
-    // flag w: wave w+1 has written its rows for wave w.  Every wave passes the one
-    // barrier below before any flag is set or read.
-    if (lane == 0) flags[w] = 0;
-    if (w == 0) {
-        stash[(3 * VS + 1) * 64 + lane] = i4v{0, 0, 0, 0};
-        if (lane == 0) flags[4] = 1;
-    }
-    __syncthreads();
-    int tx, ty, f;
-    if constexpr (GEO == 2) {
-        const int wave = blk * 4 + w;
-        if (wave >= tiles_x * chunks_y * n_fields) return;
-        vk_tile_of(wave, tiles_x, chunks_y, n_fields, ga, gb, tx, ty, f);
-    } else {
-        if (blk >= tiles_x * groups_y * n_fields) return;
-        int g;
-        vk_tile_of(blk, tiles_x, groups_y, n_fields, ga, gb, tx, g, f);
-        ty = 4 * g + w;
-        if (ty >= chunks_y) return;
-    }
-    const int c0 = out_lo + ty * rows_per_chunk;
-    const int c1 = min(c0 + rows_per_chunk, out_hi);
-    const int x0 = tx * W;
-    if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
-    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1])) {
-        PsStash X;
-        X.lane = lane;
-        // wave 0 has no wave above: its rows go to the trash row after the three areas
-        X.wr = (lds_i4v *)&stash[(w > 0 ? (w - 1) * VS : 3 * VS) * 64];
-        X.wstride = w > 0 ? 64 : 0;
-        X.wflag = (lds_flag *)&flags[w > 0 ? w - 1 : 3];
-        // the chunk below is this group's (every chunk is VS_RCH rows: launch_vs)
-        X.linked = GEO == 0 && w < 3 && ty + 1 < chunks_y;
-        X.rd = (const lds_i4v *)&stash[(X.linked ? w * VS : 3 * VS + 1) * 64];
-        X.rstride = X.linked ? 64 : 0;
-        X.rflag = (lds_flag *)&flags[X.linked ? w : 4];
-        ps_plane<K, PD, C, SC, 0, KH, W, VS>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect,
-                                             coef, c4, cK, f, x0, c0, c1, lane, X);
-    }
+                                          c4, cK, f, x0, c0, c1, lane);
     if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 
@@ -547,41 +381,6 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     }
-}
-
-template <int K, int PD, int C, int VS, int XM = 4, int GEO = 0>
-bool launch_vs(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
-               int in_lo, int in_hi, int top, int bot, double coef, const double *mm, const VkPsCouple *cp) {
-    constexpr int KH = (K + C - 1) / C * C;
-    constexpr int W = 64 * C - 2 * KH;
-    const int tiles_x = (ny + W - 1) / W;
-    const int rch = chunk_rows(out_hi - out_lo, tiles_x, nf);
-    // every chunk exactly VS_RCH rows (the kernel's row plan is fixed at compile time)
-    if (rch != VS_RCH || (out_hi - out_lo) % VS_RCH != 0) return false;
-    const int chunks_y = (out_hi - out_lo + rch - 1) / rch;
-    const int groups_y = (chunks_y + 3) / 4;
-    int ea = 0, eb = 0;
-    vk_edge_chunks(K, out_lo, out_hi, rch, chunks_y, top, bot, ea, eb);
-    // groups holding an edge chunk go first, as the edge chunks do in the wave-tile order
-    int ga = (ea + 3) / 4, gb = eb > 0 ? groups_y - (chunks_y - eb) / 4 : 0;
-    if (ga + gb > groups_y) { ga = groups_y; gb = 0; }
-    int blocks = tiles_x * groups_y * nf;
-    if (GEO == 2) { ga = ea; gb = eb; blocks = (tiles_x * chunks_y * nf + 3) / 4; }
-    const double c4 = 1.0 - 4.0 * coef;
-    VkPsCouple none = {};
-    const VkPsCouple &cpl = cp ? *cp : none;
-    if (fabs(c4) >= 1e-3) {
-        double cK = 1.0;
-        for (int k = 0; k < K; ++k) cK *= c4;
-        hipLaunchKernelGGL((k_diffuse_ps_vs<K, PD, C, true, VS, XM, GEO>), dim3(blocks), dim3(256), 0, st, src, dst, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, groups_y, nf, coef / c4, c4,
-                           cK, mm, cpl, ga, gb);
-    } else {
-        hipLaunchKernelGGL((k_diffuse_ps_vs<K, PD, C, false, VS, XM, GEO>), dim3(blocks), dim3(256), 0, st, src, dst, fs, ny,
-                           out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, groups_y, nf, coef, c4, 1.0,
-                           mm, cpl, ga, gb);
-    }
-    return true;
 }
 
 }  // namespace vk_ps

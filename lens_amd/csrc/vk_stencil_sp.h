@@ -103,8 +103,7 @@ __device__ __forceinline__ void sp_iter(SpState<K, PD, C, Stages<K, NW, S>::NS, 
     double r0c[C], r0f[C];
     if constexpr (S == 0) {
         vk_ps::ps_load<C, GL && GR && EY, CP & 1>(St.ring[(U + PD) % NR],
-                                                   A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L,
-                                                   i + PD < A.row_end);
+                                                   A.s + clamp_row(i + PD, A.in_lo, A.in_hi) * L.ny64, L);
 #pragma unroll
         for (int j = 0; j < C; ++j) {
             r0c[j] = St.ring[(U + NR - 1) % NR][j];
@@ -264,7 +263,6 @@ __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict
     A.in_hi = in_hi;
     A.top = top_reflect;
     A.bot = bot_reflect;
-    A.row_end = c1 + K;
     A.coef = coef;
     A.c4 = c4;
     A.cK = cK;

@@ -32,9 +32,6 @@ def test_stencil_kernel_names_follow_the_launch_rules():
     assert bench.stencil_kernel_name(20, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
     assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(40, 10, 'fma', whole) == 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-    assert bench.stencil_kernel_name(60, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps_vs<10, 4, 2, true, 16, 4, 0>'
-    assert bench.stencil_kernel_name(62, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps_vs<10, 4, 2, true, 17, 4, 0>'
-    assert bench.stencil_kernel_name(60, 10, 'fma', whole, False) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(40, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0>'
     assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
     assert bench.stencil_kernel_name(6, 10, 'exact') == 'vk_nt::k_diffuse_wl<10, 3, false>'
