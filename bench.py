@@ -140,10 +140,12 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
     if mode == 'fma' and depth <= 11 and (depth % 2 == 1 or depth == 10):
         if variant == 40 and depth == 10:
             return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-        # k_diffuse_ps<K, PD, C, SC, CP> (vk_stencil_ps.h); SC = the rescaled form (coef not ~1/4)
+        # k_diffuse_ps<K, PD, C, SC, CP, KHO> (vk_stencil_ps.h); SC = the rescaled form (coef not
+        # ~1/4); KHO = 16 halo columns for variant 70's line-aligned 10-deep tiles
+        kho = 16 if (variant == 70 and depth == 10) else 0
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
-            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2>'
-        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0>' % depth
+            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, %d>' % kho
+        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0, %d>' % (depth, kho)
     if depth == 10:    # the exact mode's 10-deep whole-step plan
         return 'vk_nt::k_diffuse_wl<10, 3, false>'
     if variant in (6, 20, 40) and depth in (7, 9, 11):
@@ -168,7 +170,7 @@ def parse(argv=None):
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40],
+    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40, 70],
                    help='tolerance mode: 20 = pair-sum passes (default on one GPU), 40 = the 10-deep pair-sum '
                         'pass with its stages split '
                         'over a workgroup\'s waves (default on row bands), 6 = the variant-6 FMA form; exact '
@@ -236,6 +238,12 @@ def stencil_settings(args, world):
         # against 0.447 / 0.439 / 0.434 ms, r05bm/, r05bn/; N = 8 keeps variant 40: 0.295 / 0.297
         # against 0.305 / 0.305)
         kernel = 40 if ((world > 4 or args.workload == 'c3') and args.stencil_mode == 'fma' and depth == 10) else 20
+        # the whole C4 plane: variant 70, the 10-deep pass with line-aligned tiles (96 written
+        # columns; 1.262-1.273 against 1.280-1.303 ms per C4 step, passes 1.160 against 1.188 ms
+        # per step, profiles/r06/r06l/); row bands keep theirs (N = 2 / 4 / 8: 0.693 / 0.438 /
+        # 0.315 against 0.687 / 0.432 / 0.297 ms with variant 20 / 20 / 40, r06m/)
+        if kernel == 20 and world == 1 and args.workload == 'c4' and args.stencil_mode == 'fma' and depth == 10:
+            kernel = 70
     rows = args.stencil_rows
     if rows is None:
         # 64-row tiles on the whole 4096^2 plane (64 chunks of each plane exactly): since the

@@ -80,7 +80,8 @@ int g_stencil_rows = 0;    // output rows per wave tile (vk_stencil_kernels.h ch
 // streaming stores at depths 7 / 9 / 11 (the exact mode's kernel for every other
 // setting).  Tolerance mode: 20 = pair-sum passes (vk_stencil_ps.h, the default; 2 /
 // 3 / 6 select it too), 40 = the stage-split 10-deep pass (vk_stencil_sp.h; row
-// bands).  Tolerance-mode depths without a pair-sum pass (even depths below 10, 13,
+// bands), 70 = the 10-deep pair-sum pass with line-aligned tiles (96 written columns,
+// vk_stencil_ps10.hip; the C4 default since round 6).  Tolerance-mode depths without a pair-sum pass (even depths below 10, 13,
 // 15) run the exact wave tiles.
 // Retired after A/B on the GPU: 0 (workgroup tile, LDS exchange),
 // 1 (lag-2 wave tile), 4 (9 rows prefetched), 5 (4 waves/SIMD cap, spills),
@@ -94,7 +95,7 @@ static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40)
+    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40 || variant == 70)
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;
@@ -198,7 +199,9 @@ static void launch_pass(int k, hipStream_t s, const double *src, double *dst, co
         if (g_stencil_kernel >= 40 && !strip &&
             vk_launch_sp(g_stencil_kernel, k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp))
             return;
-        if (k == 10) vk_launch_ps10(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+        if (k == 10 && g_stencil_kernel == 70 && !strip)
+            vk_launch_ps10_aligned(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
+        else if (k == 10) vk_launch_ps10(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
         else vk_launch_ps(k, s, src, dst, f0, nf, fs, ny, lo, hi, in_lo, in_hi, top, bot, coef, mm, cp);
     } else if (k == 10 || ((g_stencil_kernel == 6 || g_stencil_kernel >= 20) && (k == 7 || k == 9 || k == 11))) {
         // the exact mode's variant 6 (streaming stores), and its 10-deep whole-step plan

@@ -41,6 +41,7 @@ struct VkPsCouple {
 void vk_launch_ps(VK_STENCIL_LAUNCH_ARGS);     // tolerance mode, pair-sum form (k = 3, 5, 7, 9, 11)
 void vk_launch_ps10(VK_STENCIL_LAUNCH_ARGS);   // the same, k = 10
 void vk_launch_ps10_strips(VK_STENCIL_LAUNCH_ARGS, int gap_lo, int gap_hi);   // k = 10, two strips
+void vk_launch_ps10_aligned(VK_STENCIL_LAUNCH_ARGS);   // k = 10, 96 written columns (variant 70)
 bool vk_launch_sp(int variant, VK_STENCIL_LAUNCH_ARGS);       // variant 40-43 (k = 10); false: not taken
 
 // ---------------------------------------------------------------------------

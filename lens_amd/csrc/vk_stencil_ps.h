@@ -320,14 +320,16 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
     }
 }
 
-template <int K, int PD, int C, bool SC, int CP = 0>
+// KHO > 0: that many halo columns per side instead of the fewest whole lanes >= K
+// (KHO = 16: 96 written columns, every tile's rows 128-B-line aligned; variant 70)
+template <int K, int PD, int C, bool SC, int CP = 0, int KHO = 0>
 __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
                                                     const double *__restrict__ uniform, const VkPsCouple cp,
                                                     int gap_lo, int gap_hi, int chunks_a, int ea, int eb) {
-    constexpr int KH = (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
+    constexpr int KH = KHO > 0 ? KHO : (K + C - 1) / C * C;      // halo columns per side: >= K, whole lanes
     constexpr int W = 64 * C - 2 * KH;           // columns written per tile
     const int blk = vk_xcd_block<4>((int)blockIdx.x, (int)gridDim.x);
     const int wave = __builtin_amdgcn_readfirstlane((int)(blk * (blockDim.x >> 6) + (threadIdx.x >> 6)));
@@ -350,11 +352,11 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 
-template <int K, int PD, int C, int CP = 0>
+template <int K, int PD, int C, int CP = 0, int KHO = 0>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
             int in_lo, int in_hi, int top, int bot, double coef, const double *mm, const VkPsCouple *cp,
             int gap_lo = -1, int gap_hi = -1) {
-    constexpr int KH = (K + C - 1) / C * C;
+    constexpr int KH = KHO > 0 ? KHO : (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
     const int tiles_x = (ny + W - 1) / W;
     if (!(gap_lo >= out_lo && gap_lo <= gap_hi && gap_hi <= out_hi)) gap_lo = gap_hi = out_hi;
@@ -373,11 +375,11 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     if (fabs(c4) >= 1e-3) {
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP, KHO>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
                            out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     } else {
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP, KHO>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     }

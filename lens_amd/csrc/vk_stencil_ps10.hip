@@ -25,3 +25,17 @@ void vk_launch_ps10_strips(VK_STENCIL_LAUNCH_ARGS, int gap_lo, int gap_hi) {
     vk_ps::launch<10, 4, 2, 2>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp, gap_lo,
                                gap_hi);
 }
+
+// Variant 70: 16 halo columns per side and 96 written columns, so every tile's loads
+// and stores cover whole 128-B lines (variant 20: 10 and 108, a row's 864-B store
+// shares its end lines with the next tile's).  12 % more VALU per written cell, but
+// the C4 step's passes take 1.160 against 1.188 ms (profiles/r06/r06l/); the same
+// store-policy rule as vk_launch_ps10.
+void vk_launch_ps10_aligned(VK_STENCIL_LAUNCH_ARGS) {
+    (void)f0; (void)k;
+    const double pass_bytes = 16.0 * (double)(in_hi - in_lo) * (double)ny * (double)nf;
+    if (pass_bytes <= 192.0 * 1024 * 1024)
+        vk_ps::launch<10, 4, 2, 2, 16>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
+    else
+        vk_ps::launch<10, 4, 2, 0, 16>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
+}

@@ -10,7 +10,7 @@
 #   prof    rocprofv3 kernel trace + stats of the bench (no counters)
 #   pmc     the pass's counters (FETCH_SIZE, WRITE_SIZE, SQ), one rocprofv3 run per group, on
 #           scripts/stencil_once.py (DEPTH / ROWS / MODE / VARIANT / REPS from the environment;
-#           unset, they default to the C4 bench pass: DEPTH=10 ROWS=64 MODE=fma VARIANT=20)
+#           unset, they default to the C4 bench pass: DEPTH=10 ROWS=64 MODE=fma VARIANT=70)
 #   sweep   scripts/stencil_sweep.py with $SWEEP_ARGS
 #   cmd     $CMD under a 300 s limit (output in $O/cmd.log)
 set -o pipefail

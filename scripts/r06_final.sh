@@ -18,7 +18,10 @@ if [ "${PMC:-1}" = 1 ]; then
     timeout -s KILL 120 rocprofv3 --pmc $grp --output-format csv -d $O/pmc_$i -o run -- \
       python3 scripts/stencil_once.py > $O/pmc_$i.log 2>&1 || { echo "pmc $grp failed"; tail -5 $O/pmc_$i.log; exit 6; }
   done
-  python3 scripts/pmc_to_json.py 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0>' 33554432 10 64 20 \
+  # the bench's own kernel and settings (bench.stencil_settings / stencil_kernel_name at N = 1)
+  read KNAME VAR < <(python3 -c "import bench; a = bench.parse([]); m, d, k, r = bench.stencil_settings(a, 1); print(bench.stencil_kernel_name(k, d, m, 16.0 * 4096 * 4096 * 2).replace(' ', '~'), k)")
+  KNAME=${KNAME//\~/ }
+  python3 scripts/pmc_to_json.py "$KNAME" 33554432 10 64 $VAR \
     $O/pmc_1/run_counter_collection.csv $O/pmc_2/run_counter_collection.csv $O/pmc_stencil_ps_d10.json \
     --sq $O/pmc_3/run_counter_collection.csv --mode fma --commit $COMMIT > $O/pmc_json.log 2>&1 || { cat $O/pmc_json.log; exit 7; }
   tail -1 $O/pmc_json.log | cut -c1-300

@@ -90,6 +90,28 @@ def test_fma_mode_large_tiles_vs_c_oracle(dev, depth, rows, shape, variant):
     assert not np.array_equal(got, f0)
 
 
+@pytest.mark.parametrize('rows', [64, 34, 17])
+@pytest.mark.parametrize('shape', [(700, 1000), (333, 517), (260, 1296), (300, 96), (200, 97), (128, 200)])
+def test_aligned_tiles_bitwise_vs_variant20(dev, shape, rows):
+    """Variant 70 (the 10-deep pass with 16 halo columns, 96 written: every tile's
+    rows whole 128-B lines) computes every cell as variant 20 does, bit for bit,
+    whatever the tile grid; and within 1e-13 of the C oracle."""
+    from lens_amd.lattice import Lattice
+    rng = np.random.default_rng(13)
+    nx, ny = shape
+    f0 = rng.random((nx, ny)) + 0.5
+    got = {}
+    for variant in (70, 20):
+        with _mode('fma', 10, rows, variant):
+            lat = Lattice(['a'], (nx, ny), (float(nx), float(ny)), 10.0, 5.0, device=dev, initial={'a': f0})
+            lat.diffuse(1.0)
+            got[variant] = lat.owned('a').cpu().numpy()
+    assert np.array_equal(got[70], got[20])
+    ref = np.ascontiguousarray(f0.copy())
+    cpu.diffuse(ref, 5.0 * 0.01, 100)
+    assert _rel(got[70], ref) < TOL
+
+
 def test_depth10_full_c4_planes_vs_depth9(dev):
     """The tolerance mode's 10-deep whole-step plan (10 passes per 100 substeps,
     three buffers) against the 9-deep plan on the full 4096^2 x 2 planes, three
