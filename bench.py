@@ -195,6 +195,9 @@ def parse(argv=None):
     p.add_argument('--couple', action='store_true',
                    help='carry the gather and the exchange in the first / final diffusion pass (vk_diffuse_coupled; '
                         'same results; off by default: 1.533 vs 1.511 ms per C4 step, profiles/r04/r04h)')
+    p.add_argument('--no-exchange-in-pass', dest='exchange_in_pass', action='store_false',
+                   help='run the exchange as its own sweep after the diffusion passes instead of adding it to the '
+                        'rows the final pass stores (vk_diffuse_exchange, variant 70; same results)')
     p.add_argument('--steps-per-launch', type=int, default=None,
                    help='held colonies (C2): timesteps per kernel launch (vk_step_dopri5_multi, each step bit for '
                         'bit the one-step kernel\'s); default = the steps per replayed graph')
@@ -595,6 +598,7 @@ def run(args, rank, world, dev, dist):
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     col.fuse_coupling = bool(args.couple)
+    col.exchange_in_pass = bool(getattr(args, 'exchange_in_pass', True))
     halo_ex = allred = balancer = None
     if world > 1 and lat is not None:
         from lens_amd.distributed import make_halo_exchange, make_uniform_allreduce
@@ -929,6 +933,7 @@ def run(args, rank, world, dev, dist):
                        'exchange': args.exchange, 'parallelism': 'row-bands x%d' % world,
                        'agents_in_bin_order': bool(nx and args.sort_agents),
                        'coupled_passes': bool(args.couple and getattr(col, '_couple', None) is not None),
+                       'exchange_in_pass': bool(lat is not None and col._exchange_in_pass_ok(1.0)),
                        'stencil_mode': args.stencil_mode if nx else None,
                        'halo': (col.lattice.halo if col.lattice is not None else 0) if world > 1 else 0},
             'roofline': roofline,

@@ -268,7 +268,7 @@ int vk_diffuse_delta(double *field, double *work0, double *work1, double *delta,
  * Uniform planes (the vk_field_uniform summary in `uniform`, nullable) keep
  * their values and still gather and exchange.  Returns VK_ERR_LIMIT and launches
  * nothing unless the step is planned as two or more pair-sum passes (the
- * tolerance mode, vk_set_stencil_mode(1), with kernel variants 20-25 and pass
+ * tolerance mode, vk_set_stencil_mode(1), with kernel variants 20 / 70 and pass
  * depths 3..11; n_fields <= 8): the caller then runs the three steps itself.
  * Not a reference interface: DiffusionField.next_update (diffusion_field.py:
  * 362-407) and the agents' exchange updates (registry.py:149-183) fused.     */
@@ -278,6 +278,22 @@ int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fi
                        int64_t n_agents, const int32_t *gather_row, double *conc, int64_t conc_ld,
                        const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
                        double binvol_avogadro, vk_stream_t stream);
+
+/* vk_diffuse_coupled without the gather, the exchange added to each cell before
+ * the final pass stores it (in registers: the agents of a wave's cells are staged
+ * in LDS first) where that pass has the path -- the tolerance mode's 10-deep
+ * line-aligned pass, kernel variant 70 -- and after its stores otherwise.  The
+ * new planes equal vk_diffuse followed by vk_exchange_sorted bit for bit; the
+ * exchange sweep's re-read and re-write of the agents' lines is gone.  Same
+ * arguments, ordering requirements and VK_ERR_LIMIT rule as vk_diffuse_coupled.
+ * Replaces DiffusionField.diffuse (diffusion_field.py:385-407) followed by the
+ * agents' update_field_with_exchange (registry.py:149-183), applied by
+ * Store.apply_update in agent order (core/experiment.py:1351-1450).          */
+int vk_diffuse_exchange(double *field, double *work0, double *work1, int32_t n_fields,
+                        int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
+                        const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
+                        int64_t n_agents, const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
+                        double binvol_avogadro, vk_stream_t stream);
 
 /* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
  * 1..15; 1 = one launch per substep; or 10, the default: a block of a multiple

@@ -74,6 +74,11 @@ class Colony:
         # by default: on one MI355X at C4 the coupled step ran 1.533 ms against 1.511
         # with the separate launches (profiles/r04/r04h/couple_ab.log)
         self.fuse_coupling = False
+        # lattice colonies stored in bin order on a whole plane: the exchange added to
+        # the new planes inside the final diffusion pass, before it stores each row
+        # (vk_diffuse_exchange; same bits as the separate sweep), where that pass has
+        # the path -- the 10-deep line-aligned pass (stencil variant 70)
+        self.exchange_in_pass = True
         # lattice colonies on the specialised agent-per-lane DP45 kernel: the gather of
         # the next step's local environment rides on the kinetics launch
         # (vk_step_dopri5_gather; the same values as vk_gather right after it)
@@ -397,6 +402,8 @@ class Colony:
                    self.fuse_coupling and self._couple is not None and self.exchange_mode == 'sorted' and
                    self.lattice.coupled_plan_ok(dt))
         fused = self.lattice is not None and not coupled and self._gather_fused()
+        exin = (self.lattice is not None and not coupled and halo_done is None and halo_exchange is None and
+                self._exchange_in_pass_ok(dt))
         if fused:
             self.kinetics_and_gather(dt)                     # + the pre-step field (one-step lag)
         else:
@@ -407,6 +414,17 @@ class Colony:
             stamp(1)
         if self.lattice is not None:
             lat = self.lattice
+            if exin:
+                if not fused:
+                    self.gather_external()                   # pre-step field (one-step lag)
+                seg, _, crow = self._couple
+                if lat.diffuse_exchange(dt, self.bin_lin, self.n, seg, crow, self.counts, allreduce=allreduce,
+                                        events=timing.get('diff')):
+                    self._finish_step(dt)
+                    if stamp is not None:
+                        stamp(2)
+                    return
+                fused = True                                 # (the gather ran)
             if not (halo_done is None and halo_exchange is None and self._coupled_step(dt, allreduce, timing)):
                 if not fused:
                     self.gather_external()                   # pre-step field (one-step lag)
@@ -511,6 +529,14 @@ class Colony:
         self.flux.copy_(flux)
         self.counts.copy_(counts)
         self._step_exchange()
+
+    def _exchange_in_pass_ok(self, dt):
+        """Whether this step's exchange can ride on its final diffusion pass's stores
+        (:attr:`exchange_in_pass`, vk_diffuse_exchange)."""
+        lat = self.lattice
+        return (self.exchange_in_pass and not self.fuse_coupling and self._couple is not None and
+                self.exchange_mode == 'sorted' and self.map_exch_count.numel() > 0 and
+                native._lib.vk_set_stencil_kernel(-1, -1) == 70 and lat.coupled_plan_ok(dt))
 
     def _coupled_step(self, dt, allreduce, timing):
         """gather + diffusion + exchange as one coupled pass sequence, when the

@@ -28,7 +28,9 @@ struct VkPsCouple {
     const int32_t *seg;
     int32_t nseg;
     int32_t n;                             // agents
-    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it
+    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it,
+                                           // bit 2: exchange added to the rows before they are stored
+    int32_t rows;                          // rows of the plane (seg holds rows * nseg entries)
     double *gdst;                          // gather: gdst[grow[f] * gld + a] = plane f at bins[a] (pre-pass)
     int64_t gld;
     const int64_t *counts;                 // exchange: plane f += counts[crow[f] * cld + a] / bva * 1000

@@ -177,10 +177,101 @@ struct PsArgs {
 
 __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (int64_t)min(max(r, lo), hi - 1); }
 
+// The exchange added in registers before the final pass stores a row (VkPsCouple
+// mode bit 2; update_field_with_exchange, registry.py:149-183).  Before its
+// pipeline, a wave stages the agents of its cells -- output rows [c0, c1) x its
+// written columns, a contiguous run of the bin-ordered agents per row (cp.seg) --
+// into LDS as (lane column, counts / bva * 1000) in agent order, with a row index.
+// At each stored row the wave walks that row's entries (wave-uniform: broadcast LDS
+// reads) and the lane owning the cell adds them to it, in agent order: the bits of
+// k_exchange_sorted's v = v + ... on the stored value, without the separate sweep
+// that re-reads and re-writes the agents' lines (57 us per C4 step).  A wave whose
+// cells hold more agents than its slots (or a chunk taller than 64 rows) takes the
+// post-store path (vk_couple_exchange) instead.
+constexpr int EX_ROWS = 64;      // rows per chunk the row index holds
+constexpr int EX_CAP = 752;      // staged agents per wave: 4 waves x 12.5 KB, 3 workgroups per CU
+struct ExEntry {
+    int32_t col;                 // the cell's column in the tile (lane = col / 2, j = col % 2); -1: none
+    int32_t pad;
+    double mm;
+};
+struct ExStage {
+    int32_t rowptr[EX_ROWS + 1];
+    int32_t pad[3];
+    ExEntry e[EX_CAP];
+};
+typedef __attribute__((address_space(3))) ExStage lds_exstage;
+
+struct PsExch {
+    const lds_exstage *st;       // nullptr: no exchange at the store
+    int c0;
+    int lane;
+};
+
+// Stage this wave's agents; false (nothing staged) if they do not fit.  Lane i
+// takes row c0 + i.
+__device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, int f, int ny, int x0, int W, int KH,
+                                         int c0, int c1, int lane) {
+    const int cr = cp.crow[f];
+    if (cr < 0 || c1 - c0 > EX_ROWS) return false;
+    const int ce = min(x0 + W, ny);
+    const int r = c0 + lane;
+    int a_lo = 0, a_hi = 0;
+    if (r < c1) {
+        const int64_t base = (int64_t)r * cp.nseg;
+        a_lo = cp.seg[base + (x0 >> 4)];
+        const int s_end = (ce + 15) >> 4;
+        a_hi = s_end < cp.nseg ? cp.seg[base + s_end] : (r + 1 < cp.rows ? cp.seg[base + cp.nseg] : cp.n);
+    }
+    const int cnt = a_hi - a_lo;
+    // exclusive prefix sum of cnt over the wave
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    if (total > EX_CAP) return false;
+    const int off = incl - cnt;
+    if (lane < c1 - c0) st->rowptr[lane] = off;
+    if (lane == 0) st->rowptr[c1 - c0] = total;      // (c1 - c0 may be 64: no lane of that index)
+    const int64_t *cnts = cp.counts + (int64_t)cr * cp.cld;
+    const int rb = r * ny;
+    for (int k = 0; k < cnt; ++k) {
+        const int a = a_lo + k;
+        const int b = cp.bins[a] - rb;     // the column of the agent's bin, if in row r
+        st->e[off + k].col = (b >= x0 && b < ce) ? b - (x0 - KH) : -1;
+        st->e[off + k].mm = ((double)cnts[a] / cp.bva) * 1000.0;
+    }
+    // the wave reads what its lanes wrote (one wave: LDS keeps its order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return true;
+}
+
+// The stored row r's exchange, added to this lane's cells v[0..C-1] in agent order
+template <int C>
+__device__ __forceinline__ void ex_apply(const PsExch &X, int r, double (&v)[C]) {
+    const int lr = r - X.c0;
+    const int e0 = __builtin_amdgcn_readfirstlane(X.st->rowptr[lr]);
+    const int e1 = __builtin_amdgcn_readfirstlane(X.st->rowptr[lr + 1]);
+    const int mine = C * X.lane;
+    for (int e = e0; e < e1; ++e) {
+        const int j = X.st->e[e].col - mine;
+        const double m = X.st->e[e].mm;
+#pragma unroll
+        for (int q = 0; q < C; ++q)
+            if (j == q) v[q] = v[q] + m;
+    }
+}
+
 // Iteration i at ring phase U (row i sits in ring slot U): prefetch row i+PD,
 // run stages [0, ACT), store row i-K if STORE.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U>
-__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U, bool EX = false>
+__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i,
+                                        const PsExch &X = PsExch{}) {
     constexpr int NR = PD + 2;
     constexpr int P = U & 1;
     // keep iterations in program order: the scheduler would otherwise hoist the
@@ -212,6 +303,7 @@ __device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, c
 #pragma unroll
                 for (int j = 0; j < C; ++j) v[j] *= A.cK;
             }
+            if constexpr (EX) ex_apply<C>(X, i - K, v);
             ps_store<C, GL && GR && EY, CP>(A.d + (int64_t)(i - K) * L.ny64, v, L);
         }
     }
@@ -229,28 +321,30 @@ __device__ __forceinline__ void ps_fill(PsState<K, PD, C> &S, const PsArgs &A, c
 // The last (i1 - i) < NR iterations, nested (iteration u runs only if u-1 ran),
 // so that no state has to be merged across a skipped iteration: a flat list of
 // guarded iterations keeps both versions of every row live and costs ~60 VGPRs.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u>
-__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u, bool EX>
+__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n,
+                                        const PsExch &X) {
     constexpr int NR = PD + 2;
     if constexpr (u < NR - 1) {
         if (u < n) {
-            ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + u) % NR>(S, A, L, i + u);
-            ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, u + 1>(S, A, L, i, n);
+            ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + u) % NR, EX>(S, A, L, i + u, X);
+            ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, u + 1, EX>(S, A, L, i, n, X);
         }
     }
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int... Us>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, bool EX, int... Us>
 __device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsState<K, PD, C> &S, const PsArgs &A,
-                                          const PsLane &L, int i, int i1) {
+                                          const PsLane &L, int i, int i1, const PsExch &X) {
     constexpr int NR = PD + 2;
     constexpr int PH = (2 * K - 1) % NR;    // ring phase of the first steady iteration
-    for (; i + NR <= i1; i += NR) (ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR>(S, A, L, i + Us), ...);
-    ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, 0>(S, A, L, i, i1 - i);
+    for (; i + NR <= i1; i += NR)
+        (ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR, EX>(S, A, L, i + Us, X), ...);
+    ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, 0, EX>(S, A, L, i, i1 - i, X);
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP>
-__device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, bool EX = false>
+__device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1, const PsExch &X = PsExch{}) {
     constexpr int NR = PD + 2;
     PsState<K, PD, C> S;
 #pragma unroll
@@ -266,14 +360,15 @@ __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0
         ps_load<C, GL && GR && EY, CP>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
     ps_fill<K, PD, C, GL, GR, EY, SC, CP, 0>(S, A, L, is);
     // steady: i = c0+K .. c1+K-1, one stored row each (rows c0 .. c1-1)
-    ps_steady<K, PD, C, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);
+    ps_steady<K, PD, C, GL, GR, EY, SC, CP, EX>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K, X);
 }
 
 // The stencil work of one wave: its tile of plane f, output rows [c0, c1)
-template <int K, int PD, int C, bool SC, int CP, int KH, int W>
+template <int K, int PD, int C, bool SC, int CP, int KH, int W, bool EX = false>
 __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double *dst, int64_t field_stride, int ny,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
-                                         double c4, double cK, int f, int x0, int c0, int c1, int lane) {
+                                         double c4, double cK, int f, int x0, int c0, int c1, int lane,
+                                         const PsExch &X = PsExch{}) {
     PsLane L;
     L.ny = ny;
     L.ny64 = ny;
@@ -311,18 +406,18 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
     // fourth body for reflected rows alone (171), take it to 2 waves per SIMD.  The
     // unscaled form (coef ~ 1/4) runs the general body everywhere.
     if (!SC || ey || (gl && gr) || (ny % C) != 0)
-        ps_body<K, PD, C, true, true, true, SC, CP>(A, L, c0, c1);
+        ps_body<K, PD, C, true, true, true, SC, CP, EX>(A, L, c0, c1, X);
     else if constexpr (SC) {
         if (gl || gr)
-            ps_body<K, PD, C, true, true, false, SC, CP>(A, L, c0, c1);
+            ps_body<K, PD, C, true, true, false, SC, CP, EX>(A, L, c0, c1, X);
         else
-            ps_body<K, PD, C, false, false, false, SC, CP>(A, L, c0, c1);
+            ps_body<K, PD, C, false, false, false, SC, CP, EX>(A, L, c0, c1, X);
     }
 }
 
 // KHO > 0: that many halo columns per side instead of the fewest whole lanes >= K
 // (KHO = 16: 96 written columns, every tile's rows 128-B-line aligned; variant 70)
-template <int K, int PD, int C, bool SC, int CP = 0, int KHO = 0>
+template <int K, int PD, int C, bool SC, int CP = 0, int KHO = 0, bool EX = false>
 __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
@@ -346,13 +441,36 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
     // agent coupling: the gather reads the plane before this pass changes anything
     if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     // a uniform plane keeps its values (zero delta); the exchange still applies
-    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
-        ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
-                                          c4, cK, f, x0, c0, c1, lane);
-    if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
+    // (a kernel without the store path takes bit 2 as bit 1)
+    bool post = (cp.mode & (EX ? 2 : 6)) != 0;
+    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1])) {
+        if constexpr (EX) {
+            // the exchange in registers at the store (mode bit 2), where the wave's agents fit
+            __shared__ ExStage stage[4];
+            lds_exstage *st = (lds_exstage *)&stage[threadIdx.x >> 6];
+            if ((cp.mode & 4) && ex_stage(st, cp, f, ny, x0, W, KH, c0, c1, lane)) {
+                PsExch X;
+                X.st = st;
+                X.c0 = c0;
+                X.lane = lane;
+                ps_plane<K, PD, C, SC, CP, KH, W, true>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect,
+                                                        bot_reflect, coef, c4, cK, f, x0, c0, c1, lane, X);
+            } else {
+                post = post || (cp.mode & 4) != 0;
+                ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect,
+                                                  coef, c4, cK, f, x0, c0, c1, lane);
+            }
+        } else {
+            ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
+                                              c4, cK, f, x0, c0, c1, lane);
+        }
+    } else {
+        post = post || (cp.mode & 4) != 0;
+    }
+    if (post) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 
-template <int K, int PD, int C, int CP = 0, int KHO = 0>
+template <int K, int PD, int C, int CP = 0, int KHO = 0, bool EX = false>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
             int in_lo, int in_hi, int top, int bot, double coef, const double *mm, const VkPsCouple *cp,
             int gap_lo = -1, int gap_hi = -1) {
@@ -375,11 +493,11 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     if (fabs(c4) >= 1e-3) {
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP, KHO>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP, KHO, EX>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
                            out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     } else {
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP, KHO>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP, KHO, EX>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     }

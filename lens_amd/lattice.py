@@ -297,6 +297,31 @@ class Lattice:
             events[1].record()
         return True
 
+    def diffuse_exchange(self, timestep: float, bin_lin, n_agents: int, seg, count_rows, counts,
+                         allreduce: Optional[Callable] = None, events=None):
+        """One whole-plane step (:meth:`diffuse`) whose final pass adds the
+        exchange counts to the new planes (:meth:`exchange_sorted`) -- before it
+        stores each row where that pass has the path (variant 70), else after
+        (vk_diffuse_exchange).  Same results, requirements and False return as
+        :meth:`diffuse_coupled`, without its gather."""
+        n_sub = n_substeps(timestep, self.diffusion_dt)
+        coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
+        mm = self.uniform_summary(allreduce)
+        if events is not None:
+            events[0].record()
+        nf = len(self.molecules)
+        rc = native._lib.vk_diffuse_exchange(
+            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1), nf, self.field_stride,
+            self.ny, self.rows_local, n_sub, coeff_dt, native.ptr(mm), native.ptr(bin_lin), native.ptr(seg),
+            (self.ny + 15) // 16, int(n_agents), (ctypes.c_int32 * nf)(*count_rows), native.ptr(counts),
+            counts.shape[1], self.binvol_avogadro, native.stream_handle())
+        if rc == native.VK_ERR_LIMIT:
+            return False
+        native.check(rc, 'vk_diffuse_exchange')
+        if events is not None:
+            events[1].record()
+        return True
+
     def exchange_first_halo(self, timestep: float, halo_exchange: Callable, stream):
         """Run the halo exchange of :meth:`diffuse`'s first block on ``stream``
         (a communication stream), so it overlaps what the launch stream does
