@@ -47,11 +47,11 @@ struct Kp {  // device copy of vk_kremling_params plus host-derived constants
     int n_int, m_int; // the exponents n, m when they are small non-negative integers, else -1
 };
 
-// division with the hardware reciprocal refined by two Newton steps (the
-// integrators' dp::fdiv; tolerance-parity, like every adaptive kernel here)
+// division with the hardware reciprocal refined by one Newton step (~1e-15
+// relative; tolerance parity against odeint, like every adaptive kernel here: a
+// second step cost 6 % of the Kremling step, profiles/r06/r06t/)
 __device__ __forceinline__ double kdiv(double a, double b) {
     double r = __builtin_amdgcn_rcp(b);
-    r = fma(fma(-b, r, 1.0), r, r);
     r = fma(fma(-b, r, 1.0), r, r);
     return a * r;
 }

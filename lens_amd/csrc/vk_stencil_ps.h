@@ -189,15 +189,23 @@ __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (in
 // cells hold more agents than its slots (or a chunk taller than 64 rows) takes the
 // post-store path (vk_couple_exchange) instead.
 constexpr int EX_ROWS = 64;      // rows per chunk the row index holds
-constexpr int EX_CAP = 752;      // staged agents per wave: 4 waves x 12.5 KB, 3 workgroups per CU
+constexpr int EX_LEVELS = 4;     // agents one lane's two cells may hold in a row (more: the wave falls back)
+constexpr int EX_CAP = 576;      // staged agents per wave: 4 waves x 12.3 KB, 3 workgroups per CU
+constexpr int EX_BATCH = 8;      // agents whose loads a lane issues together while staging
 struct ExEntry {
-    int32_t col;                 // the cell's column in the tile (lane = col / 2, j = col % 2); -1: none
+    int32_t q;                   // the cell of the owning lane: 0 = its first column, 1 = its second
     int32_t pad;
-    double mm;
+    double mm;                   // counts / bva * 1000
+};
+// One row: its agents' entries are e[e0 ..], grouped by owning lane (ascending) and
+// within a lane in agent order; bit l of m[j] = lane l owns more than j of them.
+struct ExRow {
+    uint64_t m[EX_LEVELS];
+    int32_t e0;
+    int32_t pad[3];
 };
 struct ExStage {
-    int32_t rowptr[EX_ROWS + 1];
-    int32_t pad[3];
+    ExRow row[EX_ROWS];
     ExEntry e[EX_CAP];
 };
 typedef __attribute__((address_space(3))) ExStage lds_exstage;
@@ -234,15 +242,47 @@ __device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, 
     const int total = __shfl(incl, 63, 64);
     if (total > EX_CAP) return false;
     const int off = incl - cnt;
-    if (lane < c1 - c0) st->rowptr[lane] = off;
-    if (lane == 0) st->rowptr[c1 - c0] = total;      // (c1 - c0 may be 64: no lane of that index)
     const int64_t *cnts = cp.counts + (int64_t)cr * cp.cld;
     const int rb = r * ny;
-    for (int k = 0; k < cnt; ++k) {
-        const int a = a_lo + k;
-        const int b = cp.bins[a] - rb;     // the column of the agent's bin, if in row r
-        st->e[off + k].col = (b >= x0 && b < ce) ? b - (x0 - KH) : -1;
-        st->e[off + k].mm = ((double)cnts[a] / cp.bva) * 1000.0;
+    // the row's agents in bin order: those left of the tile's columns first, then the
+    // tile's (grouped by owning lane), then those right of it
+    uint64_t m[EX_LEVELS] = {};
+    int e0 = off, prev = -1, level = 0;
+    bool over = false;
+    for (int k0 = 0; k0 < cnt; k0 += EX_BATCH) {     // loads in flight together (~6 agents a row at C4)
+        int b[EX_BATCH];
+        int64_t c[EX_BATCH];
+#pragma unroll
+        for (int j = 0; j < EX_BATCH; ++j) {
+            const bool in = k0 + j < cnt;
+            b[j] = in ? cp.bins[a_lo + k0 + j] - rb : -1;     // the column of the agent's bin
+            c[j] = in ? cnts[a_lo + k0 + j] : 0;
+        }
+#pragma unroll
+        for (int j = 0; j < EX_BATCH; ++j) {
+            if (k0 + j < cnt) {
+                const int col = b[j] - (x0 - KH);               // the column in the tile
+                if (b[j] < x0) {
+                    e0 = off + k0 + j + 1;
+                } else if (b[j] < ce) {
+                    const int t = col >> 1;                     // the owning lane
+                    level = t == prev ? level + 1 : 0;
+                    prev = t;
+                    over = over || level >= EX_LEVELS;
+#pragma unroll
+                    for (int l = 0; l < EX_LEVELS; ++l)
+                        if (level == l) m[l] |= 1ull << t;
+                }
+                st->e[off + k0 + j].q = col & 1;
+                st->e[off + k0 + j].mm = ((double)c[j] / cp.bva) * 1000.0;
+            }
+        }
+    }
+    if (__any(over)) return false;
+    if (r < c1) {
+#pragma unroll
+        for (int l = 0; l < EX_LEVELS; ++l) st->row[lane].m[l] = m[l];
+        st->row[lane].e0 = e0;
     }
     // the wave reads what its lanes wrote (one wave: LDS keeps its order)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -251,19 +291,50 @@ __device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, 
     return true;
 }
 
-// The stored row r's exchange, added to this lane's cells v[0..C-1] in agent order
+__device__ __forceinline__ uint64_t ex_uniform64(uint64_t x) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
+}
+
+// popcount of the mask's bits below this lane
+__device__ __forceinline__ int ex_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// The stored row r's exchange, added to this lane's cells v[0..1] in agent order:
+// the lane's entries start after those of the lanes below it.  Every lane reads its
+// first two entries (levels 0 and 1, predicated: a row holds ~6 agents at C4 and
+// one lane in ~150 owns two); levels 2 and 3 only where a lane of the row needs them.
 template <int C>
 __device__ __forceinline__ void ex_apply(const PsExch &X, int r, double (&v)[C]) {
+    static_assert(C == 2, "two cells per lane");
     const int lr = r - X.c0;
-    const int e0 = __builtin_amdgcn_readfirstlane(X.st->rowptr[lr]);
-    const int e1 = __builtin_amdgcn_readfirstlane(X.st->rowptr[lr + 1]);
-    const int mine = C * X.lane;
-    for (int e = e0; e < e1; ++e) {
-        const int j = X.st->e[e].col - mine;
-        const double m = X.st->e[e].mm;
+    const uint64_t m0 = ex_uniform64(X.st->row[lr].m[0]);
+    const uint64_t m1 = ex_uniform64(X.st->row[lr].m[1]);
+    const uint64_t m2 = ex_uniform64(X.st->row[lr].m[2]);
+    const uint64_t m3 = ex_uniform64(X.st->row[lr].m[3]);
+    const int e0 = __builtin_amdgcn_readfirstlane(X.st->row[lr].e0);
+    const int first = e0 + ex_below(m0) + ex_below(m1) + ex_below(m2) + ex_below(m3);
+    const uint64_t bit = 1ull << X.lane;
 #pragma unroll
-        for (int q = 0; q < C; ++q)
-            if (j == q) v[q] = v[q] + m;
+    for (int l = 0; l < 2; ++l) {
+        const bool has = ((l == 0 ? m0 : m1) & bit) != 0;
+        const int e = has ? first + l : 0;
+        const int q = X.st->e[e].q;
+        const double mm = X.st->e[e].mm;
+        if (has && q == 0) v[0] = v[0] + mm;
+        if (has && q == 1) v[1] = v[1] + mm;
+    }
+    if (m2 != 0) {
+#pragma unroll
+        for (int l = 2; l < EX_LEVELS; ++l) {
+            const bool has = ((l == 2 ? m2 : m3) & bit) != 0;
+            const int e = has ? first + l : 0;
+            const int q = X.st->e[e].q;
+            const double mm = X.st->e[e].mm;
+            if (has && q == 0) v[0] = v[0] + mm;
+            if (has && q == 1) v[1] = v[1] + mm;
+        }
     }
 }
 
