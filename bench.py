@@ -170,7 +170,7 @@ def parse(argv=None):
                    help='keep the agents in their generated order instead of bin order (Colony.sort_by_bin)')
     p.add_argument('--generic-kernel', action='store_true',
                    help='use the table-walking DP45 kernel instead of the specialised one')
-    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40, 70, 75],
+    p.add_argument('--stencil-kernel', type=int, default=None, choices=[2, 3, 6, 20, 40, 70],
                    help='tolerance mode: 20 = pair-sum passes (default on one GPU), 40 = the 10-deep pair-sum '
                         'pass with its stages split '
                         'over a workgroup\'s waves (default on row bands), 6 = the variant-6 FMA form; exact '

@@ -95,7 +95,7 @@ static int g_stencil_kernel = 20;
 
 extern "C" int vk_set_stencil_kernel(int32_t variant, int32_t rows) {
     const int prev = g_stencil_kernel;
-    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40 || variant == 70 || variant == 75)
+    if (variant == 2 || variant == 3 || variant == 6 || variant == 20 || variant == 40 || variant == 70)
         g_stencil_kernel = variant;
     if (rows == 0 || (rows >= 8 && rows <= 4096)) g_stencil_rows = rows;
     return prev;

@@ -223,13 +223,13 @@ __device__ __forceinline__ void sp_dispatch(int w, int body, const PsArgs &A, co
 
 // One workgroup = one (column tile, chunk of output rows, plane).  The tile
 // mapping is the plane's: tile tx of chunk ty, chunks in row order.
-template <int K, int PD, int C, int NW, bool SC, int CP = 0, int KHO = 0>
+template <int K, int PD, int C, int NW, bool SC, int CP = 0>
 __global__ __launch_bounds__(64 * NW) void k_diffuse_sp(const double *__restrict__ src, double *dst,
                                                        int64_t field_stride, int ny, int out_lo, int out_hi, int in_lo,
                                                        int in_hi, int top_reflect, int bot_reflect, int rows_per_chunk,
                                                        int tiles_x, int chunks_y, int nf, int ea, int eb, double coef,
                                                        double c4, double cK, const double *__restrict__ uniform) {
-    constexpr int KH = KHO > 0 ? KHO : (K + C - 1) / C * C;   // KHO = 16: line-aligned tiles (variant 75)
+    constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
     constexpr int SLOTS = 2;     // hand-off slots per boundary
     __shared__ __attribute__((aligned(16))) double xfer[(NW > 1 ? NW - 1 : 1) * SLOTS * 64 * C];
@@ -313,10 +313,10 @@ inline int round_rows(int out_rows, int per_round) {
     return rows > 8 ? rows : 8;
 }
 
-template <int K, int PD, int C, int NW, int CP = 0, int KHO = 0>
+template <int K, int PD, int C, int NW, int CP = 0>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
             int in_lo, int in_hi, int top, int bot, double coef, const double *mm, int rows) {
-    constexpr int KH = KHO > 0 ? KHO : (K + C - 1) / C * C;
+    constexpr int KH = (K + C - 1) / C * C;
     constexpr int W = 64 * C - 2 * KH;
     const int tiles_x = (ny + W - 1) / W;
     if (rows <= 0) rows = round_rows(out_hi - out_lo, resident_groups<K, PD, C, NW, CP>() / (tiles_x * nf));
@@ -328,11 +328,11 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     if (fabs(c4) >= 1e-3) {
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
-        hipLaunchKernelGGL((k_diffuse_sp<K, PD, C, NW, true, CP, KHO>), dim3(groups), dim3(64 * NW), 0, st, src, dst, fs,
+        hipLaunchKernelGGL((k_diffuse_sp<K, PD, C, NW, true, CP>), dim3(groups), dim3(64 * NW), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rows, tiles_x, chunks_y, nf, ea, eb, coef / c4, c4, cK,
                            mm);
     } else {
-        hipLaunchKernelGGL((k_diffuse_sp<K, PD, C, NW, false, CP, KHO>), dim3(groups), dim3(64 * NW), 0, st, src, dst, fs,
+        hipLaunchKernelGGL((k_diffuse_sp<K, PD, C, NW, false, CP>), dim3(groups), dim3(64 * NW), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rows, tiles_x, chunks_y, nf, ea, eb, coef, c4, 1.0,
                            mm);
     }

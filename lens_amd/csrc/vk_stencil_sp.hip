@@ -13,11 +13,8 @@
 
 bool vk_launch_sp(int variant, VK_STENCIL_LAUNCH_ARGS) {
     (void)f0;
-    if ((variant != 40 && variant != 75) || k != 10 || (cp && cp->mode)) return false;
+    if (variant != 40 || k != 10 || (cp && cp->mode)) return false;
     const int rows = g_stencil_rows > 0 ? g_stencil_rows : 0;   // 0: whole rounds of workgroups (vk_sp::round_rows)
-    if (variant == 75)   // A/B: line-aligned tiles (16 halo columns, 96 written), as variant 70
-        vk_sp::launch<10, 4, 2, 5, 0, 16>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows);
-    else
-        vk_sp::launch<10, 4, 2, 5>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows);
+    vk_sp::launch<10, 4, 2, 5>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, rows);
     return true;
 }

@@ -61,7 +61,7 @@ def stencil_kernel(variant: int = -1, rows: int = -1) -> int:
     return native._lib.vk_set_stencil_kernel(int(variant), int(rows))
 
 
-STENCIL_VARIANTS = frozenset((2, 3, 6, 20, 40, 70, 75))     # vk_set_stencil_kernel (vk_lattice.hip)
+STENCIL_VARIANTS = frozenset((2, 3, 6, 20, 40, 70))     # vk_set_stencil_kernel (vk_lattice.hip)
 
 
 def stencil_mode(mode=None) -> str:
