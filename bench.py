@@ -140,12 +140,13 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
     if mode == 'fma' and depth <= 11 and (depth % 2 == 1 or depth == 10):
         if variant == 40 and depth == 10:
             return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-        # k_diffuse_ps<K, PD, C, SC, CP, KHO> (vk_stencil_ps.h); SC = the rescaled form (coef not
-        # ~1/4); KHO = 16 halo columns for variant 70's line-aligned 10-deep tiles
+        # k_diffuse_ps<K, PD, C, SC, CP, KHO, EX> (vk_stencil_ps.h); SC = the rescaled form (coef
+        # not ~1/4); KHO = 16 halo columns for variant 70's line-aligned 10-deep tiles; EX = the
+        # final pass that adds the exchange at its stores (not the timed pass)
         kho = 16 if (variant == 70 and depth == 10) else 0
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
-            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, %d>' % kho
-        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0, %d>' % (depth, kho)
+            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, %d, false>' % kho
+        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0, %d, false>' % (depth, kho)
     if depth == 10:    # the exact mode's 10-deep whole-step plan
         return 'vk_nt::k_diffuse_wl<10, 3, false>'
     if variant in (6, 20, 40) and depth in (7, 9, 11):
