@@ -37,7 +37,7 @@ from lens_amd import native
 from lens_amd.cells import CellModel, lineage_ids
 from lens_amd.configs import initial_conc
 from lens_amd.kinetics import KineticsEngine
-from lens_amd.lattice import Lattice, occupancy, segment_index, N_A_LEGACY
+from lens_amd.lattice import Lattice, occupancy, segment_index, exchange_image, N_A_LEGACY
 from lens_amd.rate_law_compiler import compile_rate_laws, RateLawTable
 
 
@@ -249,6 +249,8 @@ class Colony:
                 r[f] = x
             rows.append(r)
         self._couple = (segment_index(self.bin_lin, n, lat.rows_local, lat.ny), rows[0], rows[1])
+        # the agent layout of the exchange added in the final pass (vk_diffuse_exchange)
+        self._ex_image = exchange_image(self.bin_lin, n, lat.rows_local, lat.ny, nf, self.ld)
 
     def sort_by_bin(self):
         """Store the agents in bin order, so that the exchange scatter and the
@@ -419,7 +421,7 @@ class Colony:
                     self.gather_external()                   # pre-step field (one-step lag)
                 seg, _, crow = self._couple
                 if lat.diffuse_exchange(dt, self.bin_lin, self.n, seg, crow, self.counts, allreduce=allreduce,
-                                        events=timing.get('diff')):
+                                        events=timing.get('diff'), image=self._ex_image):
                     self._finish_step(dt)
                     if stamp is not None:
                         stamp(2)

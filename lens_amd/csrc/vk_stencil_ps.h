@@ -188,25 +188,21 @@ __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (in
 // that re-reads and re-writes the agents' lines (57 us per C4 step).  A wave whose
 // cells hold more agents than its slots (or a chunk taller than 64 rows) takes the
 // post-store path (vk_couple_exchange) instead.
-constexpr int EX_ROWS = 64;      // rows per chunk the row index holds
-constexpr int EX_LEVELS = 4;     // agents one lane's two cells may hold in a row (more: the wave falls back)
-constexpr int EX_CAP = 576;      // staged agents per wave: 4 waves x 12.3 KB, 3 workgroups per CU
-constexpr int EX_BATCH = 8;      // agents whose loads a lane issues together while staging
-struct ExEntry {
-    int32_t q;                   // the cell of the owning lane: 0 = its first column, 1 = its second
-    int32_t pad;
-    double mm;                   // counts / bva * 1000
-};
-// One row: its agents' entries are e[e0 ..], grouped by owning lane (ascending) and
-// within a lane in agent order; bit l of m[j] = lane l owns more than j of them.
+constexpr int EX_ROWS = 64;      // rows per chunk the image holds
+constexpr int EX_LEVELS = 4;     // agents one lane's two cells may hold in a row (more: the region falls back)
+constexpr int EX_CAP = 1152;     // agents per region the LDS holds: 4 waves x 12 KB, 3 workgroups per CU
+// One row of a region: its agents are entries e0 .. of the region, grouped by owning
+// lane (ascending) and within a lane in agent order; bit l of m[j] = lane l owns more
+// than j of them; bit k of qbits = the row's entry k is in its lane's second cell.
 struct ExRow {
     uint64_t m[EX_LEVELS];
+    uint64_t qbits;
     int32_t e0;
-    int32_t pad[3];
+    int32_t pad;
 };
 struct ExStage {
     ExRow row[EX_ROWS];
-    ExEntry e[EX_CAP];
+    double e[EX_CAP];
 };
 typedef __attribute__((address_space(3))) ExStage lds_exstage;
 
@@ -216,74 +212,26 @@ struct PsExch {
     int lane;
 };
 
-// Stage this wave's agents; false (nothing staged) if they do not fit.  Lane i
-// takes row c0 + i.
-__device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, int f, int ny, int x0, int W, int KH,
-                                         int c0, int c1, int lane) {
-    const int cr = cp.crow[f];
-    if (cr < 0 || c1 - c0 > EX_ROWS) return false;
-    const int ce = min(x0 + W, ny);
-    const int r = c0 + lane;
-    int a_lo = 0, a_hi = 0;
-    if (r < c1) {
-        const int64_t base = (int64_t)r * cp.nseg;
-        a_lo = cp.seg[base + (x0 >> 4)];
-        const int s_end = (ce + 15) >> 4;
-        a_hi = s_end < cp.nseg ? cp.seg[base + s_end] : (r + 1 < cp.rows ? cp.seg[base + cp.nseg] : cp.n);
+// Copy this wave's region of the exchange image into LDS (coalesced loads, no
+// dependent index chain: the image is built beforehand); false if the region takes
+// the post-store path.
+__device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, int f, int tx, int ty, int tiles_x,
+                                         int rows_per_chunk, int c0, int c1, int lane) {
+    if (cp.crow[f] < 0 || !cp.xhdr || tiles_x != cp.xtiles || rows_per_chunk != cp.xrows || c1 - c0 > EX_ROWS)
+        return false;
+    const int region = ty * tiles_x + tx;
+    if (cp.xbad[region]) return false;
+    const int o0 = cp.xoff[region], n = cp.xoff[region + 1] - o0;
+    if (n > EX_CAP) return false;
+    if (lane < c1 - c0) {
+        const int64_t *h = cp.xhdr + ((int64_t)region * EX_ROWS + lane) * 6;
+#pragma unroll
+        for (int j = 0; j < EX_LEVELS; ++j) st->row[lane].m[j] = (uint64_t)h[j];
+        st->row[lane].qbits = (uint64_t)h[4];
+        st->row[lane].e0 = (int32_t)h[5];
     }
-    const int cnt = a_hi - a_lo;
-    // exclusive prefix sum of cnt over the wave
-    int incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    const int total = __shfl(incl, 63, 64);
-    if (total > EX_CAP) return false;
-    const int off = incl - cnt;
-    const int64_t *cnts = cp.counts + (int64_t)cr * cp.cld;
-    const int rb = r * ny;
-    // the row's agents in bin order: those left of the tile's columns first, then the
-    // tile's (grouped by owning lane), then those right of it
-    uint64_t m[EX_LEVELS] = {};
-    int e0 = off, prev = -1, level = 0;
-    bool over = false;
-    for (int k0 = 0; k0 < cnt; k0 += EX_BATCH) {     // loads in flight together (~6 agents a row at C4)
-        int b[EX_BATCH];
-        int64_t c[EX_BATCH];
-#pragma unroll
-        for (int j = 0; j < EX_BATCH; ++j) {
-            const bool in = k0 + j < cnt;
-            b[j] = in ? cp.bins[a_lo + k0 + j] - rb : -1;     // the column of the agent's bin
-            c[j] = in ? cnts[a_lo + k0 + j] : 0;
-        }
-#pragma unroll
-        for (int j = 0; j < EX_BATCH; ++j) {
-            if (k0 + j < cnt) {
-                const int col = b[j] - (x0 - KH);               // the column in the tile
-                if (b[j] < x0) {
-                    e0 = off + k0 + j + 1;
-                } else if (b[j] < ce) {
-                    const int t = col >> 1;                     // the owning lane
-                    level = t == prev ? level + 1 : 0;
-                    prev = t;
-                    over = over || level >= EX_LEVELS;
-#pragma unroll
-                    for (int l = 0; l < EX_LEVELS; ++l)
-                        if (level == l) m[l] |= 1ull << t;
-                }
-                st->e[off + k0 + j].q = col & 1;
-                st->e[off + k0 + j].mm = ((double)c[j] / cp.bva) * 1000.0;
-            }
-        }
-    }
-    if (__any(over)) return false;
-    if (r < c1) {
-#pragma unroll
-        for (int l = 0; l < EX_LEVELS; ++l) st->row[lane].m[l] = m[l];
-        st->row[lane].e0 = e0;
-    }
+    const double *src = cp.ximg + (int64_t)f * cp.xld + o0;
+    for (int k = lane; k < n; k += 64) st->e[k] = src[k];
     // the wave reads what its lanes wrote (one wave: LDS keeps its order)
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -313,27 +261,26 @@ __device__ __forceinline__ void ex_apply(const PsExch &X, int r, double (&v)[C])
     const uint64_t m1 = ex_uniform64(X.st->row[lr].m[1]);
     const uint64_t m2 = ex_uniform64(X.st->row[lr].m[2]);
     const uint64_t m3 = ex_uniform64(X.st->row[lr].m[3]);
+    const uint64_t qb = ex_uniform64(X.st->row[lr].qbits);
     const int e0 = __builtin_amdgcn_readfirstlane(X.st->row[lr].e0);
-    const int first = e0 + ex_below(m0) + ex_below(m1) + ex_below(m2) + ex_below(m3);
+    const int k0 = ex_below(m0) + ex_below(m1) + ex_below(m2) + ex_below(m3);   // this lane's first, in the row
     const uint64_t bit = 1ull << X.lane;
 #pragma unroll
     for (int l = 0; l < 2; ++l) {
         const bool has = ((l == 0 ? m0 : m1) & bit) != 0;
-        const int e = has ? first + l : 0;
-        const int q = X.st->e[e].q;
-        const double mm = X.st->e[e].mm;
-        if (has && q == 0) v[0] = v[0] + mm;
-        if (has && q == 1) v[1] = v[1] + mm;
+        const double mm = X.st->e[has ? e0 + k0 + l : 0];
+        const bool q1 = (qb >> ((k0 + l) & 63)) & 1;
+        if (has && !q1) v[0] = v[0] + mm;
+        if (has && q1) v[1] = v[1] + mm;
     }
     if (m2 != 0) {
 #pragma unroll
         for (int l = 2; l < EX_LEVELS; ++l) {
             const bool has = ((l == 2 ? m2 : m3) & bit) != 0;
-            const int e = has ? first + l : 0;
-            const int q = X.st->e[e].q;
-            const double mm = X.st->e[e].mm;
-            if (has && q == 0) v[0] = v[0] + mm;
-            if (has && q == 1) v[1] = v[1] + mm;
+            const double mm = X.st->e[has ? e0 + k0 + l : 0];
+            const bool q1 = (qb >> ((k0 + l) & 63)) & 1;
+            if (has && !q1) v[0] = v[0] + mm;
+            if (has && q1) v[1] = v[1] + mm;
         }
     }
 }
@@ -519,7 +466,7 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
             // the exchange in registers at the store (mode bit 2), where the wave's agents fit
             __shared__ ExStage stage[4];
             lds_exstage *st = (lds_exstage *)&stage[threadIdx.x >> 6];
-            if ((cp.mode & 4) && ex_stage(st, cp, f, ny, x0, W, KH, c0, c1, lane)) {
+            if ((cp.mode & 4) && ex_stage(st, cp, f, tx, ty, tiles_x, rows_per_chunk, c0, c1, lane)) {
                 PsExch X;
                 X.st = st;
                 X.c0 = c0;

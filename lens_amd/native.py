@@ -110,7 +110,7 @@ _SIGS = {
     'vk_diffuse_coupled': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _f64, _vp, _vp, _vp, _i32, _i64,
                             _i32p, _vp, _i64, _i32p, _vp, _i64, _f64, _vp], ctypes.c_int),
     'vk_diffuse_exchange': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _f64, _vp, _vp, _vp, _i32, _i64,
-                             _i32p, _vp, _i64, _f64, _vp], ctypes.c_int),
+                             _i32p, _vp, _i64, _f64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp], ctypes.c_int),
     'vk_set_stencil_depth': ([_i32], ctypes.c_int),
     'vk_set_stencil_kernel': ([_i32, _i32], ctypes.c_int),
     'vk_set_stencil_mode': ([_i32], ctypes.c_int),
