@@ -75,7 +75,9 @@ CASES = {
     'tall_rows64': (200, 390, 12000, 0, 3, 64),
     'crowded': (33, 260, 2500, 90, 3, 12),
     'narrow': (30, 50, 800, 40, 3, 0),
-    'over_capacity': (128, 300, 3000, 1500, 40, 64),   # one wave's cells hold > 752 agents
+    'over_capacity': (128, 300, 3000, 1500, 40, 64),   # one region's cells hold too many agents: post-store path
+    'crowded_rows64': (128, 300, 3000, 24, 16, 64),     # up to 4 agents a lane in the image path
+    'edge_tiles_rows64': (192, 290, 5000, 0, 3, 64),    # a partial last tile (290 = 3 x 96 + 2)
 }
 
 
@@ -139,6 +141,9 @@ def test_c4_exchange_in_pass_equals_separate_sweep(dev):
     with _bench_stencil():
         a = bench.build_rank(args, 0, 1, dev)[:2]
         assert a[0]._exchange_in_pass_ok(1.0)
+        # every wave region of the bench's pass takes the image path (none falls back)
+        img = a[0]._ex_image
+        assert (img.tiles, img.rows) == (43, 64) and not bool(img.xbad.bool().any())
         a[0].step(1.0)
         torch.cuda.synchronize()
         fa = [a[1].owned(m).clone() for m in a[1].molecules]
