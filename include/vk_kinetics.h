@@ -287,13 +287,15 @@ int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fi
  * re-write of the agents' lines is gone.  Same arguments, ordering requirements
  * and VK_ERR_LIMIT rule as vk_diffuse_coupled, plus the image (xhdr nullable: no
  * image), built once per agent layout for the pass's wave regions (xrows rows x
- * one of xtiles 96-column tiles; lens_amd.lattice.exchange_image): pos[a] = agent
- * a's entry (region-major, bin order within a region), xoff[g] = region g's first
- * entry (regions + 1), xbad[g] = 1 if region g adds after its stores, xhdr = per
- * region and row {m[4], qbits, e0} (6 int64: bit l of m[j] = lane l owns more than
- * j of the row's agents, bit k of qbits = the row's entry k is its lane's second
- * cell, e0 = the row's first entry in the region).  Each call writes
- * ximg[f * xld + pos[a]] = counts / binvol_avogadro * 1000 for the exchanged planes.
+ * one of xtiles 96-column tiles; lens_amd.lattice.exchange_image): entries
+ * region-major, bin order within a region, each region starting at an even entry;
+ * inv[e] = entry e's agent (-1: padding), xoff[g] = region g's first entry
+ * (regions + 1), xbad[g] = 1 if region g adds after its stores, xhdr = per region
+ * and row {m[4], qbits, e0} (6 int64: bit l of m[j] = lane l owns more than j of
+ * the row's agents, bit k of qbits = the row's entry k is its lane's second cell,
+ * e0 = the row's first entry in the region); xld = xoff[regions] + 128.  Each call
+ * writes ximg[f * xld + e] = counts[inv[e]] / binvol_avogadro * 1000 for the
+ * exchanged planes.
  * Replaces DiffusionField.diffuse (diffusion_field.py:385-407) followed by the
  * agents' update_field_with_exchange (registry.py:149-183), applied by
  * Store.apply_update in agent order (core/experiment.py:1351-1450).          */
@@ -301,7 +303,7 @@ int vk_diffuse_exchange(double *field, double *work0, double *work1, int32_t n_f
                         int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
                         const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
                         int64_t n_agents, const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
-                        double binvol_avogadro, const int32_t *pos, const int64_t *xhdr, const int32_t *xoff,
+                        double binvol_avogadro, const int32_t *inv, const int64_t *xhdr, const int32_t *xoff,
                         const uint8_t *xbad, double *ximg, int64_t xld, int32_t xtiles, int32_t xrows,
                         vk_stream_t stream);
 

@@ -250,7 +250,7 @@ class Colony:
             rows.append(r)
         self._couple = (segment_index(self.bin_lin, n, lat.rows_local, lat.ny), rows[0], rows[1])
         # the agent layout of the exchange added in the final pass (vk_diffuse_exchange)
-        self._ex_image = exchange_image(self.bin_lin, n, lat.rows_local, lat.ny, nf, self.ld)
+        self._ex_image = exchange_image(self.bin_lin, n, lat.rows_local, lat.ny, nf)
 
     def sort_by_bin(self):
         """Store the agents in bin order, so that the exchange scatter and the

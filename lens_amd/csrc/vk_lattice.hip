@@ -443,7 +443,7 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
 // VK_ERR_LIMIT, launching nothing, when the step is not planned as two or more
 // fused passes.
 struct VkExImage {
-    const int32_t *pos;
+    const int32_t *inv;
     const int64_t *xhdr;
     const int32_t *xoff;
     const uint8_t *xbad;
@@ -473,33 +473,36 @@ extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, i
                         false, nullptr, stream);
 }
 
-// The exchange image's entries of one step: ximg[f * xld + pos[a]] = counts[crow[f] *
-// cld + a] / bva * 1000 (exchange_mM's expression, the same bits) for every exchanged plane
-__global__ __launch_bounds__(256) void k_exchange_image(const int32_t *__restrict__ pos, int64_t n,
+// The exchange image's entries of one step, in entry order (coalesced stores; the
+// agents of one region row are consecutive, so the count loads mostly are too):
+// ximg[f * xld + e] = counts[crow[f] * cld + inv[e]] / bva * 1000 (exchange_mM's
+// expression, the same bits) for every exchanged plane; 0 at padding entries
+__global__ __launch_bounds__(256) void k_exchange_image(const int32_t *__restrict__ inv, int64_t n_entries,
                                                         const int64_t *__restrict__ counts, int64_t cld, VkPsCouple cp,
                                                         int n_fields, double *__restrict__ ximg, int64_t xld) {
-    const int64_t a = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (a >= n) return;
-    const int64_t p = pos[a];
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_entries) return;
+    const int a = inv[e];
     for (int f = 0; f < n_fields; ++f)
-        if (cp.crow[f] >= 0) ximg[(int64_t)f * xld + p] = ((double)counts[(int64_t)cp.crow[f] * cld + a] / cp.bva) * 1000.0;
+        if (cp.crow[f] >= 0)
+            ximg[(int64_t)f * xld + e] = a >= 0 ? ((double)counts[(int64_t)cp.crow[f] * cld + a] / cp.bva) * 1000.0 : 0.0;
 }
 
 extern "C" int vk_diffuse_exchange(double *field, double *work0, double *work1, int32_t n_fields,
                                    int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
                                    const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
                                    int64_t n_agents, const int32_t *count_row, const int64_t *counts,
-                                   int64_t counts_ld, double binvol_avogadro, const int32_t *pos, const int64_t *xhdr,
+                                   int64_t counts_ld, double binvol_avogadro, const int32_t *inv, const int64_t *xhdr,
                                    const int32_t *xoff, const uint8_t *xbad, double *ximg, int64_t xld,
                                    int32_t xtiles, int32_t xrows, vk_stream_t stream) {
     if (!count_row || n_fields < 1 || n_fields > VK_COUPLE_MAX_FIELDS ||
-        (xhdr && (!pos || !xoff || !xbad || !ximg || xld < n_agents || xtiles < 1 || xrows < 1))) {
+        (xhdr && (!inv || !xoff || !xbad || !ximg || xld < n_agents + 128 || xtiles < 1 || xrows < 1))) {
         vk::set_error("vk_diffuse_exchange: bad arguments");
         return VK_ERR_ARG;
     }
     int32_t none[VK_COUPLE_MAX_FIELDS];
     for (int f = 0; f < VK_COUPLE_MAX_FIELDS; ++f) none[f] = -1;
-    VkExImage img = {pos, xhdr, xoff, xbad, ximg, xld, xtiles, xrows};
+    VkExImage img = {inv, xhdr, xoff, xbad, ximg, xld, xtiles, xrows};
     return coupled_impl(field, work0, work1, n_fields, field_stride, ny, rows, n_sub, coeff_dt, uniform, bin_lin, seg,
                         nseg, n_agents, none, nullptr, 0, count_row, counts, counts_ld, binvol_avogadro, true,
                         xhdr ? &img : nullptr, stream);
@@ -565,8 +568,9 @@ static int coupled_impl(double *field, double *work0, double *work1, int32_t n_f
         cp.xld = img->xld;
         cp.xtiles = img->xtiles;
         cp.xrows = img->xrows;
-        hipLaunchKernelGGL(k_exchange_image, dim3((unsigned)((n_agents + 255) / 256)), dim3(256), 0, s, img->pos,
-                           n_agents, counts, counts_ld, cp, n_fields, img->ximg, img->xld);
+        const int64_t n_entries = img->xld - 128;   // the image rows' 1 KB of slack (lattice.exchange_image)
+        hipLaunchKernelGGL(k_exchange_image, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, s, img->inv,
+                           n_entries, counts, counts_ld, cp, n_fields, img->ximg, img->xld);
         const int rc = vk::launch_check("k_exchange_image");
         if (rc) return rc;
     }

@@ -212,9 +212,11 @@ struct PsExch {
     int lane;
 };
 
-// Copy this wave's region of the exchange image into LDS (coalesced loads, no
-// dependent index chain: the image is built beforehand); false if the region takes
-// the post-store path.
+// Copy this wave's region of the exchange image into LDS by LDS-DMA (global_load_lds,
+// 16 B per lane: no VGPRs, and the copy runs beside the pass's own first row loads --
+// the fill's first wait on them retires it too: loads complete in issue order); false
+// if the region takes the post-store path.  Regions start at 16-B multiples of the
+// image and each image row carries 1 KB of slack, so whole 1-KB pieces stay in bounds.
 __device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, int f, int tx, int ty, int tiles_x,
                                          int rows_per_chunk, int c0, int c1, int lane) {
     if (cp.crow[f] < 0 || !cp.xhdr || tiles_x != cp.xtiles || rows_per_chunk != cp.xrows || c1 - c0 > EX_ROWS)
@@ -223,19 +225,14 @@ __device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, 
     if (cp.xbad[region]) return false;
     const int o0 = cp.xoff[region], n = cp.xoff[region + 1] - o0;
     if (n > EX_CAP) return false;
-    if (lane < c1 - c0) {
-        const int64_t *h = cp.xhdr + ((int64_t)region * EX_ROWS + lane) * 6;
+    typedef __attribute__((address_space(3))) void lds_void;
+    const char *h = (const char *)(cp.xhdr + (int64_t)region * EX_ROWS * 6);
 #pragma unroll
-        for (int j = 0; j < EX_LEVELS; ++j) st->row[lane].m[j] = (uint64_t)h[j];
-        st->row[lane].qbits = (uint64_t)h[4];
-        st->row[lane].e0 = (int32_t)h[5];
-    }
-    const double *src = cp.ximg + (int64_t)f * cp.xld + o0;
-    for (int k = lane; k < n; k += 64) st->e[k] = src[k];
-    // the wave reads what its lanes wrote (one wave: LDS keeps its order)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = 0; j < (int)sizeof(st->row) / 1024; ++j)
+        __builtin_amdgcn_global_load_lds((const void *)(h + j * 1024 + lane * 16), (lds_void *)((char __attribute__((address_space(3))) *)st->row + j * 1024), 16, 0, 0);
+    const char *src = (const char *)(cp.ximg + (int64_t)f * cp.xld + o0);
+    for (int j = 0; j < (n + 127) / 128; ++j)
+        __builtin_amdgcn_global_load_lds((const void *)(src + j * 1024 + lane * 16), (lds_void *)((char __attribute__((address_space(3))) *)st->e + j * 1024), 16, 0, 0);
     return true;
 }
 

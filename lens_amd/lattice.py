@@ -315,7 +315,7 @@ class Lattice:
             self.ny, self.rows_local, n_sub, coeff_dt, native.ptr(mm), native.ptr(bin_lin), native.ptr(seg),
             (self.ny + 15) // 16, int(n_agents), (ctypes.c_int32 * nf)(*count_rows), native.ptr(counts),
             counts.shape[1], self.binvol_avogadro,
-            native.ptr(image.pos) if image else None, native.ptr(image.xhdr) if image else None,
+            native.ptr(image.inv) if image else None, native.ptr(image.xhdr) if image else None,
             native.ptr(image.xoff) if image else None, native.ptr(image.xbad) if image else None,
             native.ptr(image.ximg) if image else None, image.ximg.shape[1] if image else 0,
             image.tiles if image else 0, image.rows if image else 0, native.stream_handle())
@@ -472,12 +472,12 @@ EX_TILE_W, EX_HALO = 96, 16                   # variant 70's written columns and
 class ExchangeImage:
     """The agent layout of vk_diffuse_exchange's image (see :func:`exchange_image`)."""
 
-    def __init__(self, pos, xhdr, xoff, xbad, ximg, tiles, rows):
-        self.pos, self.xhdr, self.xoff, self.xbad, self.ximg = pos, xhdr, xoff, xbad, ximg
+    def __init__(self, inv, xhdr, xoff, xbad, ximg, tiles, rows):
+        self.inv, self.xhdr, self.xoff, self.xbad, self.ximg = inv, xhdr, xoff, xbad, ximg
         self.tiles, self.rows = tiles, rows
 
 
-def exchange_image(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int, n_fields: int, capacity: int,
+def exchange_image(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int, n_fields: int,
                    chunk_rows: int = EX_ROWS) -> ExchangeImage:
     """The static part of the exchange image the final pass of vk_diffuse_exchange
     reads (include/vk_kinetics.h): the agents (stored in bin order) grouped by the
@@ -499,17 +499,21 @@ def exchange_image(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int, n_f
     region = ty * tiles + tx
     colt = c - tx * EX_TILE_W + EX_HALO                  # the column in the tile: lane = colt // 2
     order = torch.sort(region, stable=True).indices     # bin order within a region (agents are in bin order)
-    pos = torch.empty(n, dtype=torch.int32, device=dev)
-    pos[order] = torch.arange(n, dtype=torch.int32, device=dev)
     per = torch.bincount(region, minlength=regions)
+    # each region starts at a 16-B multiple of the image (the pass copies it by 16-B LDS-DMA)
     xoff = torch.zeros(regions + 1, dtype=i64, device=dev)
-    xoff[1:] = torch.cumsum(per, 0)
+    xoff[1:] = torch.cumsum((per + 1) // 2 * 2, 0)
     reg_s = region[order]
+    first = torch.zeros(regions + 1, dtype=i64, device=dev)
+    first[1:] = torch.cumsum(per, 0)
+    slot = xoff[reg_s] + torch.arange(n, dtype=i64, device=dev) - first[reg_s]
+    inv = torch.full((int(xoff[-1]),), -1, dtype=torch.int32, device=dev)    # entry -> agent (-1: padding)
+    inv[slot] = order.to(torch.int32)
     rowkey = reg_s * chunk_rows + (r - ty * chunk_rows)[order]
     lane_s = (colt // 2)[order]
     q_s = (colt % 2)[order]
     idx = torch.arange(n, dtype=i64, device=dev)
-    k = idx - xoff[reg_s]                                # entry within the region
+    k = idx - first[reg_s]                               # entry within the region
     nrow = regions * chunk_rows
     e0 = torch.zeros(nrow, dtype=i64, device=dev)
     if n:
@@ -533,8 +537,9 @@ def exchange_image(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int, n_f
     sel = (q_s == 1) & (kr < 64)
     hdr[:, 4].scatter_add_(0, rowkey[sel], one[sel] << kr[sel])
     hdr[:, 5] = e0
-    ximg = torch.zeros((n_fields, max(capacity, n)), dtype=torch.float64, device=dev)
-    return ExchangeImage(pos, hdr.contiguous(), xoff.to(torch.int32), bad.to(torch.uint8), ximg, tiles, chunk_rows)
+    # each plane's row of entries with 1 KB of slack (the pass copies whole 1-KB pieces)
+    ximg = torch.zeros((n_fields, int(xoff[-1]) + 128), dtype=torch.float64, device=dev)
+    return ExchangeImage(inv, hdr.contiguous(), xoff.to(torch.int32), bad.to(torch.uint8), ximg, tiles, chunk_rows)
 
 
 def occupancy(bin_lin: torch.Tensor, n_agents: int, order_key: Optional[torch.Tensor] = None):

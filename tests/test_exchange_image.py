@@ -24,16 +24,16 @@ def _layout(rows, ny, n, seed, crowd=0):
                                              (130, 200, 2000, 9)])
 def test_exchange_image_matches_restatement(rows, ny, n, crowd):
     bins = _layout(rows, ny, n, 3, crowd)
-    img = exchange_image(torch.from_numpy(bins), n, rows, ny, 2, n + 5)
+    img = exchange_image(torch.from_numpy(bins), n, rows, ny, 2)
     tiles = (ny + EX_TILE_W - 1) // EX_TILE_W
     chunks = (rows + 63) // 64
     assert (img.tiles, img.rows) == (tiles, 64)
-    pos = img.pos.numpy()
+    inv = img.inv.numpy()
     xoff = img.xoff.numpy()
     hdr = img.xhdr.numpy().view(np.uint64).reshape(-1, 6)
     bad = img.xbad.numpy()
-    assert sorted(pos.tolist()) == list(range(n))
-    assert img.ximg.shape == (2, n + 5)
+    assert sorted(a for a in inv.tolist() if a >= 0) == list(range(n))
+    assert np.all(xoff % 2 == 0) and img.ximg.shape == (2, int(xoff[-1]) + 128)
     groups = {}
     for a, bb in enumerate(bins.tolist()):
         r, c = divmod(bb, ny)
@@ -41,9 +41,9 @@ def test_exchange_image_matches_restatement(rows, ny, n, crowd):
         groups.setdefault(g, []).append((a, r % 64, c - (c // EX_TILE_W) * EX_TILE_W + EX_HALO))
     for g in range(tiles * chunks):
         members = groups.get(g, [])
-        assert xoff[g + 1] - xoff[g] == len(members)
-        # bin order within the region
-        assert [pos[a] - xoff[g] for a, _, _ in members] == list(range(len(members)))
+        assert xoff[g + 1] - xoff[g] == len(members) + (len(members) & 1)
+        # bin order within the region, then padding
+        assert inv[xoff[g]:xoff[g + 1]].tolist() == [a for a, _, _ in members] + [-1] * (len(members) & 1)
         expect_bad = len(members) > EX_CAP
         for lr in range(64):
             row = [(k, colt) for k, (a, rr, colt) in enumerate(members) if rr == lr]
