@@ -189,34 +189,30 @@ __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (in
 // cells hold more agents than its slots (or a chunk taller than 64 rows) takes the
 // post-store path (vk_couple_exchange) instead.
 constexpr int EX_ROWS = 64;      // rows per chunk the image holds
-constexpr int EX_LEVELS = 4;     // agents one lane's two cells may hold in a row (more: the region falls back)
-constexpr int EX_CAP = 1152;     // agents per region the LDS holds: 4 waves x 12 KB, 3 workgroups per CU
-// One row of a region: its agents are entries e0 .. of the region, grouped by owning
-// lane (ascending) and within a lane in agent order; bit l of m[j] = lane l owns more
-// than j of them; bit k of qbits = the row's entry k is in its lane's second cell.
-struct ExRow {
-    uint64_t m[EX_LEVELS];
-    uint64_t qbits;
-    int32_t e0;
-    int32_t pad;
-};
+constexpr int EX_LEVELS = 3;     // agents one lane's two cells may hold in a row (more: the region falls back)
+constexpr int EX_CAP = 1152;     // agents per region the LDS holds: 4 waves x 9.5 KB, 3 workgroups per CU
+// One row of a region in the image (global memory, read with scalar loads): its agents
+// are entries e0 .. of the region, grouped by owning lane (ascending) and within a
+// lane in agent order; bit l of m[j] = lane l owns more than j of them; bit k of
+// qbits = the row's entry k is in its lane's second cell.  (m[3] is unused.)
 struct ExStage {
-    ExRow row[EX_ROWS];
-    double e[EX_CAP];
+    double e[EX_CAP + 128];      // the region's entries; the slack keeps every lane's reads in range
 };
 typedef __attribute__((address_space(3))) ExStage lds_exstage;
 
 struct PsExch {
     const lds_exstage *st;       // nullptr: no exchange at the store
+    const int64_t *hdr;          // the region's row headers (6 int64 each)
     int c0;
     int lane;
 };
 
-// Copy this wave's region of the exchange image into LDS by LDS-DMA (global_load_lds,
-// 16 B per lane: no VGPRs, and the copy runs beside the pass's own first row loads --
-// the fill's first wait on them retires it too: loads complete in issue order); false
-// if the region takes the post-store path.  Regions start at 16-B multiples of the
-// image and each image row carries 1 KB of slack, so whole 1-KB pieces stay in bounds.
+// Copy this wave's region of the exchange image's entries into LDS by LDS-DMA
+// (global_load_lds, 16 B per lane: no VGPRs, and the copy runs beside the pass's own
+// first row loads -- the fill's first wait on them retires it too: loads complete in
+// issue order); false if the region takes the post-store path.  Regions start at
+// 16-B multiples of the image and each image row carries 1 KB of slack, so whole
+// 1-KB pieces stay in bounds.
 __device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, int f, int tx, int ty, int tiles_x,
                                          int rows_per_chunk, int c0, int c1, int lane) {
     if (cp.crow[f] < 0 || !cp.xhdr || tiles_x != cp.xtiles || rows_per_chunk != cp.xrows || c1 - c0 > EX_ROWS)
@@ -226,19 +222,12 @@ __device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, 
     const int o0 = cp.xoff[region], n = cp.xoff[region + 1] - o0;
     if (n > EX_CAP) return false;
     typedef __attribute__((address_space(3))) void lds_void;
-    const char *h = (const char *)(cp.xhdr + (int64_t)region * EX_ROWS * 6);
-#pragma unroll
-    for (int j = 0; j < (int)sizeof(st->row) / 1024; ++j)
-        __builtin_amdgcn_global_load_lds((const void *)(h + j * 1024 + lane * 16), (lds_void *)((char __attribute__((address_space(3))) *)st->row + j * 1024), 16, 0, 0);
+    typedef __attribute__((address_space(3))) char lds_char;
     const char *src = (const char *)(cp.ximg + (int64_t)f * cp.xld + o0);
     for (int j = 0; j < (n + 127) / 128; ++j)
-        __builtin_amdgcn_global_load_lds((const void *)(src + j * 1024 + lane * 16), (lds_void *)((char __attribute__((address_space(3))) *)st->e + j * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *)(src + j * 1024 + lane * 16), (lds_void *)((lds_char *)st->e + j * 1024),
+                                         16, 0, 0);
     return true;
-}
-
-__device__ __forceinline__ uint64_t ex_uniform64(uint64_t x) {
-    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32);
 }
 
 // popcount of the mask's bits below this lane
@@ -246,39 +235,25 @@ __device__ __forceinline__ int ex_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
-// The stored row r's exchange, added to this lane's cells v[0..1] in agent order:
-// the lane's entries start after those of the lanes below it.  Every lane reads its
-// first two entries (levels 0 and 1, predicated: a row holds ~6 agents at C4 and
-// one lane in ~150 owns two); levels 2 and 3 only where a lane of the row needs them.
+// The stored row r's exchange, added to this lane's cells v[0..1] in agent order: the
+// lane's entries start after those of the lanes below it.  Branch-free: at each level
+// every lane reads an entry and adds it, or -0.0 (x + -0.0 = x for every x), to one of
+// its cells; the header comes through the scalar cache (uniform, no VGPRs, no LDS).
 template <int C>
 __device__ __forceinline__ void ex_apply(const PsExch &X, int r, double (&v)[C]) {
     static_assert(C == 2, "two cells per lane");
-    const int lr = r - X.c0;
-    const uint64_t m0 = ex_uniform64(X.st->row[lr].m[0]);
-    const uint64_t m1 = ex_uniform64(X.st->row[lr].m[1]);
-    const uint64_t m2 = ex_uniform64(X.st->row[lr].m[2]);
-    const uint64_t m3 = ex_uniform64(X.st->row[lr].m[3]);
-    const uint64_t qb = ex_uniform64(X.st->row[lr].qbits);
-    const int e0 = __builtin_amdgcn_readfirstlane(X.st->row[lr].e0);
-    const int k0 = ex_below(m0) + ex_below(m1) + ex_below(m2) + ex_below(m3);   // this lane's first, in the row
-    const uint64_t bit = 1ull << X.lane;
+    typedef const __attribute__((address_space(4))) int64_t c64;
+    c64 *h = (c64 *)(X.hdr + (int64_t)(r - X.c0) * 6);
+    const uint64_t m0 = (uint64_t)h[0], m1 = (uint64_t)h[1], m2 = (uint64_t)h[2], qb = (uint64_t)h[4];
+    const int e0 = (int)h[5];
+    const int k0 = ex_below(m0) + ex_below(m1) + ex_below(m2);   // this lane's first entry in the row
 #pragma unroll
-    for (int l = 0; l < 2; ++l) {
-        const bool has = ((l == 0 ? m0 : m1) & bit) != 0;
-        const double mm = X.st->e[has ? e0 + k0 + l : 0];
+    for (int l = 0; l < EX_LEVELS; ++l) {
+        const double mm = X.st->e[e0 + k0 + l];
+        const double a = ps_sel(l == 0 ? m0 : (l == 1 ? m1 : m2), mm, -0.0);
         const bool q1 = (qb >> ((k0 + l) & 63)) & 1;
-        if (has && !q1) v[0] = v[0] + mm;
-        if (has && q1) v[1] = v[1] + mm;
-    }
-    if (m2 != 0) {
-#pragma unroll
-        for (int l = 2; l < EX_LEVELS; ++l) {
-            const bool has = ((l == 2 ? m2 : m3) & bit) != 0;
-            const double mm = X.st->e[has ? e0 + k0 + l : 0];
-            const bool q1 = (qb >> ((k0 + l) & 63)) & 1;
-            if (has && !q1) v[0] = v[0] + mm;
-            if (has && q1) v[1] = v[1] + mm;
-        }
+        v[0] = v[0] + (q1 ? -0.0 : a);
+        v[1] = v[1] + (q1 ? a : -0.0);
     }
 }
 
@@ -433,7 +408,7 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
 // KHO > 0: that many halo columns per side instead of the fewest whole lanes >= K
 // (KHO = 16: 96 written columns, every tile's rows 128-B-line aligned; variant 70)
 template <int K, int PD, int C, bool SC, int CP = 0, int KHO = 0, bool EX = false>
-__global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
@@ -466,6 +441,7 @@ __global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ s
             if ((cp.mode & 4) && ex_stage(st, cp, f, tx, ty, tiles_x, rows_per_chunk, c0, c1, lane)) {
                 PsExch X;
                 X.st = st;
+                X.hdr = cp.xhdr + (int64_t)(ty * tiles_x + tx) * EX_ROWS * 6;
                 X.c0 = c0;
                 X.lane = lane;
                 ps_plane<K, PD, C, SC, CP, KH, W, true>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect,

@@ -465,7 +465,7 @@ def segment_index(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int) -> t
     return torch.searchsorted(bin_lin[:n_agents].to(torch.int64), targets).to(torch.int32)
 
 
-EX_ROWS, EX_LEVELS, EX_CAP = 64, 4, 1152      # vk_stencil_ps.h: the exchange image's region rows, levels, LDS slots
+EX_ROWS, EX_LEVELS, EX_CAP = 64, 3, 1152      # vk_stencil_ps.h: the exchange image's region rows, levels, LDS slots
 EX_TILE_W, EX_HALO = 96, 16                   # variant 70's written columns and halo columns per side
 
 
