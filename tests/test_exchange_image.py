@@ -67,7 +67,7 @@ def test_exchange_image_matches_restatement(rows, ny, n, crowd):
                 if colt % 2:
                     qbits |= 1 << kr
             if not expect_bad:
-                assert [int(x) for x in h[:4]] == masks
+                assert [int(x) for x in h[:4]] == masks + [0] * (4 - EX_LEVELS)
                 assert int(h[4]) == qbits
                 # a lane's first entry = e0 + the entries of the lanes below it
                 for lane in count:
