@@ -142,9 +142,9 @@ def test_c4_exchange_in_pass_equals_separate_sweep(dev):
         a = bench.build_rank(args, 0, 1, dev)[:2]
         assert a[0]._exchange_in_pass_ok(1.0)
         # the bench's wave regions take the image path: only regions with a lane owning
-        # five agents or more fall back (about one in 2,752 at this density)
+        # four agents of a row fall back (about one in 40 at this density)
         img = a[0]._ex_image
-        assert (img.tiles, img.rows) == (43, 64) and int(img.xbad.sum()) <= 3
+        assert (img.tiles, img.rows) == (43, 64) and int(img.xbad.sum()) <= 0.05 * img.xbad.numel()
         a[0].step(1.0)
         torch.cuda.synchronize()
         fa = [a[1].owned(m).clone() for m in a[1].molecules]
