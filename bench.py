@@ -140,13 +140,12 @@ def stencil_kernel_name(variant, depth, mode='exact', pass_bytes=None):
     if mode == 'fma' and depth <= 11 and (depth % 2 == 1 or depth == 10):
         if variant == 40 and depth == 10:
             return 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-        # k_diffuse_ps<K, PD, C, SC, CP, KHO, EX> (vk_stencil_ps.h); SC = the rescaled form (coef
-        # not ~1/4); KHO = 16 halo columns for variant 70's line-aligned 10-deep tiles; EX = the
-        # final pass that adds the exchange at its stores (not the timed pass)
+        # k_diffuse_ps<K, PD, C, SC, CP, KHO> (vk_stencil_ps.h); SC = the rescaled form (coef not
+        # ~1/4); KHO = 16 halo columns for variant 70's line-aligned 10-deep tiles
         kho = 16 if (variant == 70 and depth == 10) else 0
         if depth == 10 and pass_bytes is not None and pass_bytes <= 192 * 1024 * 1024:
-            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, %d, false>' % kho
-        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0, %d, false>' % (depth, kho)
+            return 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, %d>' % kho
+        return 'vk_ps::k_diffuse_ps<%d, 4, 2, true, 0, %d>' % (depth, kho)
     if depth == 10:    # the exact mode's 10-deep whole-step plan
         return 'vk_nt::k_diffuse_wl<10, 3, false>'
     if variant in (6, 20, 40) and depth in (7, 9, 11):
@@ -196,9 +195,6 @@ def parse(argv=None):
     p.add_argument('--couple', action='store_true',
                    help='carry the gather and the exchange in the first / final diffusion pass (vk_diffuse_coupled; '
                         'same results; off by default: 1.533 vs 1.511 ms per C4 step, profiles/r04/r04h)')
-    p.add_argument('--no-exchange-in-pass', dest='exchange_in_pass', action='store_false',
-                   help='run the exchange as its own sweep after the diffusion passes instead of adding it to the '
-                        'rows the final pass stores (vk_diffuse_exchange, variant 70; same results)')
     p.add_argument('--steps-per-launch', type=int, default=None,
                    help='held colonies (C2): timesteps per kernel launch (vk_step_dopri5_multi, each step bit for '
                         'bit the one-step kernel\'s); default = the steps per replayed graph')
@@ -599,7 +595,6 @@ def run(args, rank, world, dev, dist):
     stencil_kernel(args.stencil_kernel, args.stencil_rows)
     col, lat, host_state = build_rank(args, rank, world, dev)
     col.fuse_coupling = bool(args.couple)
-    col.exchange_in_pass = bool(getattr(args, 'exchange_in_pass', True))
     halo_ex = allred = balancer = None
     if world > 1 and lat is not None:
         from lens_amd.distributed import make_halo_exchange, make_uniform_allreduce
@@ -934,7 +929,6 @@ def run(args, rank, world, dev, dist):
                        'exchange': args.exchange, 'parallelism': 'row-bands x%d' % world,
                        'agents_in_bin_order': bool(nx and args.sort_agents),
                        'coupled_passes': bool(args.couple and getattr(col, '_couple', None) is not None),
-                       'exchange_in_pass': bool(lat is not None and col._exchange_in_pass_ok(1.0)),
                        'stencil_mode': args.stencil_mode if nx else None,
                        'halo': (col.lattice.halo if col.lattice is not None else 0) if world > 1 else 0},
             'roofline': roofline,

@@ -279,34 +279,6 @@ int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fi
                        const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
                        double binvol_avogadro, vk_stream_t stream);
 
-/* vk_diffuse_coupled without the gather, the exchange added to each cell before
- * the final pass stores it (in registers) where that pass has the path -- the
- * tolerance mode's 10-deep line-aligned pass, kernel variant 70 -- and an exchange
- * image is given, and after its stores otherwise.  The new planes equal vk_diffuse
- * followed by vk_exchange_sorted bit for bit; the exchange sweep's re-read and
- * re-write of the agents' lines is gone.  Same arguments, ordering requirements
- * and VK_ERR_LIMIT rule as vk_diffuse_coupled, plus the image (xhdr nullable: no
- * image), built once per agent layout for the pass's wave regions (xrows rows x
- * one of xtiles 96-column tiles; lens_amd.lattice.exchange_image): entries
- * region-major, bin order within a region, each region starting at an even entry;
- * inv[e] = entry e's agent (-1: padding), xoff[g] = region g's first entry
- * (regions + 1), xbad[g] = 1 if region g adds after its stores, xhdr = per region
- * and row {m[4], qbits, e0} (6 int64: bit l of m[j] = lane l owns more than j of
- * the row's agents, bit k of qbits = the row's entry k is its lane's second cell,
- * e0 = the row's first entry in the region); xld = xoff[regions] + 128.  Each call
- * writes ximg[f * xld + e] = counts[inv[e]] / binvol_avogadro * 1000 for the
- * exchanged planes.
- * Replaces DiffusionField.diffuse (diffusion_field.py:385-407) followed by the
- * agents' update_field_with_exchange (registry.py:149-183), applied by
- * Store.apply_update in agent order (core/experiment.py:1351-1450).          */
-int vk_diffuse_exchange(double *field, double *work0, double *work1, int32_t n_fields,
-                        int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
-                        const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
-                        int64_t n_agents, const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
-                        double binvol_avogadro, const int32_t *inv, const int64_t *xhdr, const int32_t *xoff,
-                        const uint8_t *xbad, double *ximg, int64_t xld, int32_t xtiles, int32_t xrows,
-                        vk_stream_t stream);
-
 /* Maximum substeps fused per HBM pass by vk_diffuse (temporal blocking; odd,
  * 1..15; 1 = one launch per substep; or 10, the default: a block of a multiple
  * of 10 substeps as 10-deep passes -- in the tolerance mode over three buffers

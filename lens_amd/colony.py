@@ -37,7 +37,7 @@ from lens_amd import native
 from lens_amd.cells import CellModel, lineage_ids
 from lens_amd.configs import initial_conc
 from lens_amd.kinetics import KineticsEngine
-from lens_amd.lattice import Lattice, occupancy, segment_index, exchange_image, N_A_LEGACY
+from lens_amd.lattice import Lattice, occupancy, segment_index, N_A_LEGACY
 from lens_amd.rate_law_compiler import compile_rate_laws, RateLawTable
 
 
@@ -74,11 +74,6 @@ class Colony:
         # by default: on one MI355X at C4 the coupled step ran 1.533 ms against 1.511
         # with the separate launches (profiles/r04/r04h/couple_ab.log)
         self.fuse_coupling = False
-        # lattice colonies stored in bin order on a whole plane: the exchange added to
-        # the new planes inside the final diffusion pass, before it stores each row
-        # (vk_diffuse_exchange; same bits as the separate sweep), where that pass has
-        # the path -- the 10-deep line-aligned pass (stencil variant 70)
-        self.exchange_in_pass = True
         # lattice colonies on the specialised agent-per-lane DP45 kernel: the gather of
         # the next step's local environment rides on the kinetics launch
         # (vk_step_dopri5_gather; the same values as vk_gather right after it)
@@ -249,8 +244,6 @@ class Colony:
                 r[f] = x
             rows.append(r)
         self._couple = (segment_index(self.bin_lin, n, lat.rows_local, lat.ny), rows[0], rows[1])
-        # the agent layout of the exchange added in the final pass (vk_diffuse_exchange)
-        self._ex_image = exchange_image(self.bin_lin, n, lat.rows_local, lat.ny, nf)
 
     def sort_by_bin(self):
         """Store the agents in bin order, so that the exchange scatter and the
@@ -404,8 +397,6 @@ class Colony:
                    self.fuse_coupling and self._couple is not None and self.exchange_mode == 'sorted' and
                    self.lattice.coupled_plan_ok(dt))
         fused = self.lattice is not None and not coupled and self._gather_fused()
-        exin = (self.lattice is not None and not coupled and halo_done is None and halo_exchange is None and
-                self._exchange_in_pass_ok(dt))
         if fused:
             self.kinetics_and_gather(dt)                     # + the pre-step field (one-step lag)
         else:
@@ -416,17 +407,6 @@ class Colony:
             stamp(1)
         if self.lattice is not None:
             lat = self.lattice
-            if exin:
-                if not fused:
-                    self.gather_external()                   # pre-step field (one-step lag)
-                seg, _, crow = self._couple
-                if lat.diffuse_exchange(dt, self.bin_lin, self.n, seg, crow, self.counts, allreduce=allreduce,
-                                        events=timing.get('diff'), image=self._ex_image):
-                    self._finish_step(dt)
-                    if stamp is not None:
-                        stamp(2)
-                    return
-                fused = True                                 # (the gather ran)
             if not (halo_done is None and halo_exchange is None and self._coupled_step(dt, allreduce, timing)):
                 if not fused:
                     self.gather_external()                   # pre-step field (one-step lag)
@@ -531,14 +511,6 @@ class Colony:
         self.flux.copy_(flux)
         self.counts.copy_(counts)
         self._step_exchange()
-
-    def _exchange_in_pass_ok(self, dt):
-        """Whether this step's exchange can ride on its final diffusion pass's stores
-        (:attr:`exchange_in_pass`, vk_diffuse_exchange)."""
-        lat = self.lattice
-        return (self.exchange_in_pass and not self.fuse_coupling and self._couple is not None and
-                self.exchange_mode == 'sorted' and self.map_exch_count.numel() > 0 and
-                native._lib.vk_set_stencil_kernel(-1, -1) == 70 and lat.coupled_plan_ok(dt))
 
     def _coupled_step(self, dt, allreduce, timing):
         """gather + diffusion + exchange as one coupled pass sequence, when the

@@ -442,78 +442,12 @@ static int diffuse_impl(double *field, double *work0, double *work1, int32_t n_f
 // while the final pass holds them).  Either arithmetic mode.  Returns
 // VK_ERR_LIMIT, launching nothing, when the step is not planned as two or more
 // fused passes.
-struct VkExImage {
-    const int32_t *inv;
-    const int64_t *xhdr;
-    const int32_t *xoff;
-    const uint8_t *xbad;
-    double *ximg;
-    int64_t xld;
-    int32_t xtiles, xrows;
-};
-
-// store_exchange: the final pass adds the exchange to its rows before storing them
-// (VkPsCouple bit 2) where its kernel has that path -- the 10-deep line-aligned pass
-// (variant 70) -- and after its stores otherwise
-static int coupled_impl(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
-                        int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt, const double *uniform,
-                        const int32_t *bin_lin, const int32_t *seg, int32_t nseg, int64_t n_agents,
-                        const int32_t *gather_row, double *conc, int64_t conc_ld, const int32_t *count_row,
-                        const int64_t *counts, int64_t counts_ld, double binvol_avogadro, bool store_exchange,
-                        const struct VkExImage *img, vk_stream_t stream);
-
 extern "C" int vk_diffuse_coupled(double *field, double *work0, double *work1, int32_t n_fields,
                                   int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
                                   const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
                                   int64_t n_agents, const int32_t *gather_row, double *conc, int64_t conc_ld,
                                   const int32_t *count_row, const int64_t *counts, int64_t counts_ld,
                                   double binvol_avogadro, vk_stream_t stream) {
-    return coupled_impl(field, work0, work1, n_fields, field_stride, ny, rows, n_sub, coeff_dt, uniform, bin_lin, seg,
-                        nseg, n_agents, gather_row, conc, conc_ld, count_row, counts, counts_ld, binvol_avogadro,
-                        false, nullptr, stream);
-}
-
-// The exchange image's entries of one step, in entry order (coalesced stores; the
-// agents of one region row are consecutive, so the count loads mostly are too):
-// ximg[f * xld + e] = counts[crow[f] * cld + inv[e]] / bva * 1000 (exchange_mM's
-// expression, the same bits) for every exchanged plane; 0 at padding entries
-__global__ __launch_bounds__(256) void k_exchange_image(const int32_t *__restrict__ inv, int64_t n_entries,
-                                                        const int64_t *__restrict__ counts, int64_t cld, VkPsCouple cp,
-                                                        int n_fields, double *__restrict__ ximg, int64_t xld) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n_entries) return;
-    const int a = inv[e];
-    for (int f = 0; f < n_fields; ++f)
-        if (cp.crow[f] >= 0)
-            ximg[(int64_t)f * xld + e] = a >= 0 ? ((double)counts[(int64_t)cp.crow[f] * cld + a] / cp.bva) * 1000.0 : 0.0;
-}
-
-extern "C" int vk_diffuse_exchange(double *field, double *work0, double *work1, int32_t n_fields,
-                                   int64_t field_stride, int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt,
-                                   const double *uniform, const int32_t *bin_lin, const int32_t *seg, int32_t nseg,
-                                   int64_t n_agents, const int32_t *count_row, const int64_t *counts,
-                                   int64_t counts_ld, double binvol_avogadro, const int32_t *inv, const int64_t *xhdr,
-                                   const int32_t *xoff, const uint8_t *xbad, double *ximg, int64_t xld,
-                                   int32_t xtiles, int32_t xrows, vk_stream_t stream) {
-    if (!count_row || n_fields < 1 || n_fields > VK_COUPLE_MAX_FIELDS ||
-        (xhdr && (!inv || !xoff || !xbad || !ximg || xld < n_agents + 128 || xtiles < 1 || xrows < 1))) {
-        vk::set_error("vk_diffuse_exchange: bad arguments");
-        return VK_ERR_ARG;
-    }
-    int32_t none[VK_COUPLE_MAX_FIELDS];
-    for (int f = 0; f < VK_COUPLE_MAX_FIELDS; ++f) none[f] = -1;
-    VkExImage img = {inv, xhdr, xoff, xbad, ximg, xld, xtiles, xrows};
-    return coupled_impl(field, work0, work1, n_fields, field_stride, ny, rows, n_sub, coeff_dt, uniform, bin_lin, seg,
-                        nseg, n_agents, none, nullptr, 0, count_row, counts, counts_ld, binvol_avogadro, true,
-                        xhdr ? &img : nullptr, stream);
-}
-
-static int coupled_impl(double *field, double *work0, double *work1, int32_t n_fields, int64_t field_stride,
-                        int32_t ny, int32_t rows, int32_t n_sub, double coeff_dt, const double *uniform,
-                        const int32_t *bin_lin, const int32_t *seg, int32_t nseg, int64_t n_agents,
-                        const int32_t *gather_row, double *conc, int64_t conc_ld, const int32_t *count_row,
-                        const int64_t *counts, int64_t counts_ld, double binvol_avogadro, bool store_exchange,
-                        const VkExImage *img, vk_stream_t stream) {
     if (!field || !work0 || !work1 || n_fields < 1 || ny <= 0 || rows <= 0 || n_sub < 0 ||
         (int64_t)rows * ny > field_stride || (int64_t)rows * ny >= INT32_MAX || n_agents < 0 ||
         n_agents >= INT32_MAX || nseg != (ny + 15) / 16 || (n_agents > 0 && (!bin_lin || !seg)) || !gather_row ||
@@ -531,7 +465,6 @@ static int coupled_impl(double *field, double *work0, double *work1, int32_t n_f
     cp.counts = counts;
     cp.cld = counts_ld;
     cp.bva = binvol_avogadro;
-    cp.rows = rows;
     if (n_fields <= VK_COUPLE_MAX_FIELDS) {
         for (int f = 0; f < n_fields; ++f) {
             if (gather_row[f] >= 127 || count_row[f] >= 127 || (gather_row[f] >= 0 && (!conc || conc_ld < n_agents)) ||
@@ -559,21 +492,6 @@ static int coupled_impl(double *field, double *work0, double *work1, int32_t n_f
         return VK_ERR_LIMIT;
     }
     hipStream_t s = (hipStream_t)stream;
-    const bool at_store = store_exchange && ten && g_stencil_kernel == 70 && img;   // vk_launch_ps10_aligned
-    if (at_store && n_agents > 0) {
-        cp.xhdr = img->xhdr;
-        cp.xoff = img->xoff;
-        cp.xbad = img->xbad;
-        cp.ximg = img->ximg;
-        cp.xld = img->xld;
-        cp.xtiles = img->xtiles;
-        cp.xrows = img->xrows;
-        const int64_t n_entries = img->xld - 128;   // the image rows' 1 KB of slack (lattice.exchange_image)
-        hipLaunchKernelGGL(k_exchange_image, dim3((unsigned)((n_entries + 255) / 256)), dim3(256), 0, s, img->inv,
-                           n_entries, counts, counts_ld, cp, n_fields, img->ximg, img->xld);
-        const int rc = vk::launch_check("k_exchange_image");
-        if (rc) return rc;
-    }
     const int np = (int)ks.size();
     const double *cur = field;
     for (int p = 0, j = 0; p < np; j += ks[p], ++p) {
@@ -583,7 +501,7 @@ static int coupled_impl(double *field, double *work0, double *work1, int32_t n_f
         else if (ten) dst = cur == work0 ? work1 : work0;
         else dst = (j + ks[p] - 1) & 1 ? work1 : work0;   // work[e & 1], e = this pass's last substep
         VkPsCouple c = cp;
-        c.mode = n_agents > 0 ? (p == 0 ? 1 : 0) | (last ? (at_store ? 4 : 2) : 0) : 0;
+        c.mode = n_agents > 0 ? (p == 0 ? 1 : 0) | (last ? 2 : 0) : 0;
         // the exact mode's final pass re-reads the step-start plane: vk_diffuse's f0
         launch_pass(ks[p], s, cur, dst, last ? field : nullptr, n_fields, field_stride, ny, 0, rows, 0, rows, 0,
                     rows - 1, coeff_dt, uniform, &c);

@@ -28,18 +28,7 @@ struct VkPsCouple {
     const int32_t *seg;
     int32_t nseg;
     int32_t n;                             // agents
-    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it,
-                                           // bit 2: exchange added to the rows before they are stored
-    int32_t rows;                          // rows of the plane (seg holds rows * nseg entries)
-    // bit 2's exchange image (vk_exchange_image_build; vk_stencil_ps.h ExRow): per wave
-    // region (xrows rows x one 96-column tile) its rows' headers, and per plane the agents'
-    // counts / bva * 1000 in region order
-    const int64_t *xhdr;                   // [regions * xrows * 6] (ExRow)
-    const int32_t *xoff;                   // [regions + 1] the first entry of each region
-    const uint8_t *xbad;                   // [regions] 1: the region takes the post-store path
-    const double *ximg;                    // ximg[f * xld + entry]
-    int64_t xld;
-    int32_t xtiles, xrows;                 // the image's geometry (the pass must match it)
+    int32_t mode;                          // bit 0: gather before the pass, bit 1: exchange after it
     double *gdst;                          // gather: gdst[grow[f] * gld + a] = plane f at bins[a] (pre-pass)
     int64_t gld;
     const int64_t *counts;                 // exchange: plane f += counts[crow[f] * cld + a] / bva * 1000

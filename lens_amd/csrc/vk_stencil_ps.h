@@ -177,91 +177,10 @@ struct PsArgs {
 
 __device__ __forceinline__ int64_t clamp_row(int r, int lo, int hi) { return (int64_t)min(max(r, lo), hi - 1); }
 
-// The exchange added in registers before the final pass stores a row (VkPsCouple
-// mode bit 2; update_field_with_exchange, registry.py:149-183).  Before its
-// pipeline, a wave stages the agents of its cells -- output rows [c0, c1) x its
-// written columns, a contiguous run of the bin-ordered agents per row (cp.seg) --
-// into LDS as (lane column, counts / bva * 1000) in agent order, with a row index.
-// At each stored row the wave walks that row's entries (wave-uniform: broadcast LDS
-// reads) and the lane owning the cell adds them to it, in agent order: the bits of
-// k_exchange_sorted's v = v + ... on the stored value, without the separate sweep
-// that re-reads and re-writes the agents' lines (57 us per C4 step).  A wave whose
-// cells hold more agents than its slots (or a chunk taller than 64 rows) takes the
-// post-store path (vk_couple_exchange) instead.
-constexpr int EX_ROWS = 64;      // rows per chunk the image holds
-constexpr int EX_LEVELS = 3;     // agents one lane's two cells may hold in a row (more: the region falls back)
-constexpr int EX_CAP = 1152;     // agents per region the LDS holds: 4 waves x 9.5 KB, 3 workgroups per CU
-// One row of a region in the image (global memory, read with scalar loads): its agents
-// are entries e0 .. of the region, grouped by owning lane (ascending) and within a
-// lane in agent order; bit l of m[j] = lane l owns more than j of them; bit k of
-// qbits = the row's entry k is in its lane's second cell.  (m[3] is unused.)
-struct ExStage {
-    double e[EX_CAP + 128];      // the region's entries; the slack keeps every lane's reads in range
-};
-typedef __attribute__((address_space(3))) ExStage lds_exstage;
-
-struct PsExch {
-    const lds_exstage *st;       // nullptr: no exchange at the store
-    const int64_t *hdr;          // the region's row headers (6 int64 each)
-    int c0;
-    int lane;
-};
-
-// Copy this wave's region of the exchange image's entries into LDS by LDS-DMA
-// (global_load_lds, 16 B per lane: no VGPRs, and the copy runs beside the pass's own
-// first row loads -- the fill's first wait on them retires it too: loads complete in
-// issue order); false if the region takes the post-store path.  Regions start at
-// 16-B multiples of the image and each image row carries 1 KB of slack, so whole
-// 1-KB pieces stay in bounds.
-__device__ __forceinline__ bool ex_stage(lds_exstage *st, const VkPsCouple &cp, int f, int tx, int ty, int tiles_x,
-                                         int rows_per_chunk, int c0, int c1, int lane) {
-    if (cp.crow[f] < 0 || !cp.xhdr || tiles_x != cp.xtiles || rows_per_chunk != cp.xrows || c1 - c0 > EX_ROWS)
-        return false;
-    const int region = ty * tiles_x + tx;
-    if (cp.xbad[region]) return false;
-    const int o0 = cp.xoff[region], n = cp.xoff[region + 1] - o0;
-    if (n > EX_CAP) return false;
-    typedef __attribute__((address_space(3))) void lds_void;
-    typedef __attribute__((address_space(3))) char lds_char;
-    const char *src = (const char *)(cp.ximg + (int64_t)f * cp.xld + o0);
-    for (int j = 0; j < (n + 127) / 128; ++j)
-        __builtin_amdgcn_global_load_lds((const void *)(src + j * 1024 + lane * 16), (lds_void *)((lds_char *)st->e + j * 1024),
-                                         16, 0, 0);
-    return true;
-}
-
-// popcount of the mask's bits below this lane
-__device__ __forceinline__ int ex_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-}
-
-// The stored row r's exchange, added to this lane's cells v[0..1] in agent order: the
-// lane's entries start after those of the lanes below it.  Branch-free: at each level
-// every lane reads an entry and adds it, or -0.0 (x + -0.0 = x for every x), to one of
-// its cells; the header comes through the scalar cache (uniform, no VGPRs, no LDS).
-template <int C>
-__device__ __forceinline__ void ex_apply(const PsExch &X, int r, double (&v)[C]) {
-    static_assert(C == 2, "two cells per lane");
-    typedef const __attribute__((address_space(4))) int64_t c64;
-    c64 *h = (c64 *)(X.hdr + (int64_t)(r - X.c0) * 6);
-    const uint64_t m0 = (uint64_t)h[0], m1 = (uint64_t)h[1], m2 = (uint64_t)h[2], qb = (uint64_t)h[4];
-    const int e0 = (int)h[5];
-    const int k0 = ex_below(m0) + ex_below(m1) + ex_below(m2);   // this lane's first entry in the row
-#pragma unroll
-    for (int l = 0; l < EX_LEVELS; ++l) {
-        const double mm = X.st->e[e0 + k0 + l];
-        const double a = ps_sel(l == 0 ? m0 : (l == 1 ? m1 : m2), mm, -0.0);
-        const bool q1 = (qb >> ((k0 + l) & 63)) & 1;
-        v[0] = v[0] + (q1 ? -0.0 : a);
-        v[1] = v[1] + (q1 ? a : -0.0);
-    }
-}
-
 // Iteration i at ring phase U (row i sits in ring slot U): prefetch row i+PD,
 // run stages [0, ACT), store row i-K if STORE.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U, bool EX = false>
-__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i,
-                                        const PsExch &X = PsExch{}) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int ACT, bool STORE, int U>
+__device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i) {
     constexpr int NR = PD + 2;
     constexpr int P = U & 1;
     // keep iterations in program order: the scheduler would otherwise hoist the
@@ -293,7 +212,6 @@ __device__ __forceinline__ void ps_iter(PsState<K, PD, C> &S, const PsArgs &A, c
 #pragma unroll
                 for (int j = 0; j < C; ++j) v[j] *= A.cK;
             }
-            if constexpr (EX) ex_apply<C>(X, i - K, v);
             ps_store<C, GL && GR && EY, CP>(A.d + (int64_t)(i - K) * L.ny64, v, L);
         }
     }
@@ -311,30 +229,28 @@ __device__ __forceinline__ void ps_fill(PsState<K, PD, C> &S, const PsArgs &A, c
 // The last (i1 - i) < NR iterations, nested (iteration u runs only if u-1 ran),
 // so that no state has to be merged across a skipped iteration: a flat list of
 // guarded iterations keeps both versions of every row live and costs ~60 VGPRs.
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u, bool EX>
-__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n,
-                                        const PsExch &X) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int PH, int u>
+__device__ __forceinline__ void ps_tail(PsState<K, PD, C> &S, const PsArgs &A, const PsLane &L, int i, int n) {
     constexpr int NR = PD + 2;
     if constexpr (u < NR - 1) {
         if (u < n) {
-            ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + u) % NR, EX>(S, A, L, i + u, X);
-            ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, u + 1, EX>(S, A, L, i, n, X);
+            ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + u) % NR>(S, A, L, i + u);
+            ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, u + 1>(S, A, L, i, n);
         }
     }
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, bool EX, int... Us>
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, int... Us>
 __device__ __forceinline__ void ps_steady(std::integer_sequence<int, Us...>, PsState<K, PD, C> &S, const PsArgs &A,
-                                          const PsLane &L, int i, int i1, const PsExch &X) {
+                                          const PsLane &L, int i, int i1) {
     constexpr int NR = PD + 2;
     constexpr int PH = (2 * K - 1) % NR;    // ring phase of the first steady iteration
-    for (; i + NR <= i1; i += NR)
-        (ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR, EX>(S, A, L, i + Us, X), ...);
-    ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, 0, EX>(S, A, L, i, i1 - i, X);
+    for (; i + NR <= i1; i += NR) (ps_iter<K, PD, C, GL, GR, EY, SC, CP, K, true, (PH + Us) % NR>(S, A, L, i + Us), ...);
+    ps_tail<K, PD, C, GL, GR, EY, SC, CP, PH, 0>(S, A, L, i, i1 - i);
 }
 
-template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP, bool EX = false>
-__device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1, const PsExch &X = PsExch{}) {
+template <int K, int PD, int C, bool GL, bool GR, bool EY, bool SC, int CP>
+__device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0, int c1) {
     constexpr int NR = PD + 2;
     PsState<K, PD, C> S;
 #pragma unroll
@@ -350,15 +266,14 @@ __device__ __forceinline__ void ps_body(const PsArgs &A, const PsLane &L, int c0
         ps_load<C, GL && GR && EY, CP>(S.ring[u], A.s + clamp_row(is + u, A.in_lo, A.in_hi) * L.ny64, L);
     ps_fill<K, PD, C, GL, GR, EY, SC, CP, 0>(S, A, L, is);
     // steady: i = c0+K .. c1+K-1, one stored row each (rows c0 .. c1-1)
-    ps_steady<K, PD, C, GL, GR, EY, SC, CP, EX>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K, X);
+    ps_steady<K, PD, C, GL, GR, EY, SC, CP>(std::make_integer_sequence<int, NR>(), S, A, L, c0 + K, c1 + K);
 }
 
 // The stencil work of one wave: its tile of plane f, output rows [c0, c1)
-template <int K, int PD, int C, bool SC, int CP, int KH, int W, bool EX = false>
+template <int K, int PD, int C, bool SC, int CP, int KH, int W>
 __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double *dst, int64_t field_stride, int ny,
                                          int in_lo, int in_hi, int top_reflect, int bot_reflect, double coef,
-                                         double c4, double cK, int f, int x0, int c0, int c1, int lane,
-                                         const PsExch &X = PsExch{}) {
+                                         double c4, double cK, int f, int x0, int c0, int c1, int lane) {
     PsLane L;
     L.ny = ny;
     L.ny64 = ny;
@@ -396,19 +311,19 @@ __device__ __forceinline__ void ps_plane(const double *__restrict__ src, double 
     // fourth body for reflected rows alone (171), take it to 2 waves per SIMD.  The
     // unscaled form (coef ~ 1/4) runs the general body everywhere.
     if (!SC || ey || (gl && gr) || (ny % C) != 0)
-        ps_body<K, PD, C, true, true, true, SC, CP, EX>(A, L, c0, c1, X);
+        ps_body<K, PD, C, true, true, true, SC, CP>(A, L, c0, c1);
     else if constexpr (SC) {
         if (gl || gr)
-            ps_body<K, PD, C, true, true, false, SC, CP, EX>(A, L, c0, c1, X);
+            ps_body<K, PD, C, true, true, false, SC, CP>(A, L, c0, c1);
         else
-            ps_body<K, PD, C, false, false, false, SC, CP, EX>(A, L, c0, c1, X);
+            ps_body<K, PD, C, false, false, false, SC, CP>(A, L, c0, c1);
     }
 }
 
 // KHO > 0: that many halo columns per side instead of the fewest whole lanes >= K
 // (KHO = 16: 96 written columns, every tile's rows 128-B-line aligned; variant 70)
-template <int K, int PD, int C, bool SC, int CP = 0, int KHO = 0, bool EX = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
+template <int K, int PD, int C, bool SC, int CP = 0, int KHO = 0>
+__global__ __launch_bounds__(256) void k_diffuse_ps(const double *__restrict__ src, double *dst, int64_t field_stride,
                                                     int ny, int out_lo, int out_hi, int in_lo, int in_hi,
                                                     int top_reflect, int bot_reflect, int rows_per_chunk, int tiles_x,
                                                     int chunks_y, int n_fields, double coef, double c4, double cK,
@@ -431,37 +346,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // agent coupling: the gather reads the plane before this pass changes anything
     if (cp.mode & 1) vk_couple_gather(cp, src + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
     // a uniform plane keeps its values (zero delta); the exchange still applies
-    // (a kernel without the store path takes bit 2 as bit 1)
-    bool post = (cp.mode & (EX ? 2 : 6)) != 0;
-    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1])) {
-        if constexpr (EX) {
-            // the exchange in registers at the store (mode bit 2), where the wave's agents fit
-            __shared__ ExStage stage[4];
-            lds_exstage *st = (lds_exstage *)&stage[threadIdx.x >> 6];
-            if ((cp.mode & 4) && ex_stage(st, cp, f, tx, ty, tiles_x, rows_per_chunk, c0, c1, lane)) {
-                PsExch X;
-                X.st = st;
-                X.hdr = cp.xhdr + (int64_t)(ty * tiles_x + tx) * EX_ROWS * 6;
-                X.c0 = c0;
-                X.lane = lane;
-                ps_plane<K, PD, C, SC, CP, KH, W, true>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect,
-                                                        bot_reflect, coef, c4, cK, f, x0, c0, c1, lane, X);
-            } else {
-                post = post || (cp.mode & 4) != 0;
-                ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect,
-                                                  coef, c4, cK, f, x0, c0, c1, lane);
-            }
-        } else {
-            ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
-                                              c4, cK, f, x0, c0, c1, lane);
-        }
-    } else {
-        post = post || (cp.mode & 4) != 0;
-    }
-    if (post) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
+    if (!(uniform && uniform[2 * f] == uniform[2 * f + 1]))
+        ps_plane<K, PD, C, SC, CP, KH, W>(src, dst, field_stride, ny, in_lo, in_hi, top_reflect, bot_reflect, coef,
+                                          c4, cK, f, x0, c0, c1, lane);
+    if (cp.mode & 2) vk_couple_exchange(cp, dst + (int64_t)f * field_stride, f, ny, x0, W, c0, c1, lane);
 }
 
-template <int K, int PD, int C, int CP = 0, int KHO = 0, bool EX = false>
+template <int K, int PD, int C, int CP = 0, int KHO = 0>
 void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, int ny, int out_lo, int out_hi,
             int in_lo, int in_hi, int top, int bot, double coef, const double *mm, const VkPsCouple *cp,
             int gap_lo = -1, int gap_hi = -1) {
@@ -484,11 +375,11 @@ void launch(hipStream_t st, const double *src, double *dst, int nf, int64_t fs, 
     if (fabs(c4) >= 1e-3) {
         double cK = 1.0;
         for (int k = 0; k < K; ++k) cK *= c4;
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP, KHO, EX>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, true, CP, KHO>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs, ny,
                            out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef / c4, c4, cK, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     } else {
-        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP, KHO, EX>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
+        hipLaunchKernelGGL((k_diffuse_ps<K, PD, C, false, CP, KHO>), dim3((waves + 3) / 4), dim3(256), 0, st, src, dst, fs,
                            ny, out_lo, out_hi, in_lo, in_hi, top, bot, rch, tiles_x, chunks_y, nf, coef, c4, 1.0, mm, cpl,
                            gap_lo, gap_hi, chunks_a, ea, eb);
     }

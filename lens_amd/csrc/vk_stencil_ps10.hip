@@ -34,16 +34,7 @@ void vk_launch_ps10_strips(VK_STENCIL_LAUNCH_ARGS, int gap_lo, int gap_hi) {
 void vk_launch_ps10_aligned(VK_STENCIL_LAUNCH_ARGS) {
     (void)f0; (void)k;
     const double pass_bytes = 16.0 * (double)(in_hi - in_lo) * (double)ny * (double)nf;
-    if (cp && (cp->mode & 4)) {
-        // the final pass of a coupled step with the exchange added at the store (its own
-        // instantiation: the staging's LDS stays out of every other pass)
-        if (pass_bytes <= 192.0 * 1024 * 1024)
-            vk_ps::launch<10, 4, 2, 2, 16, true>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm,
-                                                 cp);
-        else
-            vk_ps::launch<10, 4, 2, 0, 16, true>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm,
-                                                 cp);
-    } else if (pass_bytes <= 192.0 * 1024 * 1024)
+    if (pass_bytes <= 192.0 * 1024 * 1024)
         vk_ps::launch<10, 4, 2, 2, 16>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);
     else
         vk_ps::launch<10, 4, 2, 0, 16>(st, src, dst, nf, fs, ny, out_lo, out_hi, in_lo, in_hi, top, bot, coef, mm, cp);

@@ -297,35 +297,6 @@ class Lattice:
             events[1].record()
         return True
 
-    def diffuse_exchange(self, timestep: float, bin_lin, n_agents: int, seg, count_rows, counts,
-                         allreduce: Optional[Callable] = None, events=None, image: Optional[ExchangeImage] = None):
-        """One whole-plane step (:meth:`diffuse`) whose final pass adds the
-        exchange counts to the new planes (:meth:`exchange_sorted`) -- before it
-        stores each row where that pass has the path (variant 70), else after
-        (vk_diffuse_exchange).  Same results, requirements and False return as
-        :meth:`diffuse_coupled`, without its gather."""
-        n_sub = n_substeps(timestep, self.diffusion_dt)
-        coeff_dt = self.diffusion * min(timestep, self.diffusion_dt)
-        mm = self.uniform_summary(allreduce)
-        if events is not None:
-            events[0].record()
-        nf = len(self.molecules)
-        rc = native._lib.vk_diffuse_exchange(
-            native.ptr(self.fields), native.ptr(self.work0), native.ptr(self.work1), nf, self.field_stride,
-            self.ny, self.rows_local, n_sub, coeff_dt, native.ptr(mm), native.ptr(bin_lin), native.ptr(seg),
-            (self.ny + 15) // 16, int(n_agents), (ctypes.c_int32 * nf)(*count_rows), native.ptr(counts),
-            counts.shape[1], self.binvol_avogadro,
-            native.ptr(image.inv) if image else None, native.ptr(image.xhdr) if image else None,
-            native.ptr(image.xoff) if image else None, native.ptr(image.xbad) if image else None,
-            native.ptr(image.ximg) if image else None, image.ximg.shape[1] if image else 0,
-            image.tiles if image else 0, image.rows if image else 0, native.stream_handle())
-        if rc == native.VK_ERR_LIMIT:
-            return False
-        native.check(rc, 'vk_diffuse_exchange')
-        if events is not None:
-            events[1].record()
-        return True
-
     def exchange_first_halo(self, timestep: float, halo_exchange: Callable, stream):
         """Run the halo exchange of :meth:`diffuse`'s first block on ``stream``
         (a communication stream), so it overlaps what the launch stream does
@@ -463,83 +434,6 @@ def segment_index(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int) -> t
     targets = (torch.arange(rows, dtype=torch.int64, device=dev)[:, None] * ny +
                16 * torch.arange(nseg, dtype=torch.int64, device=dev)[None, :]).reshape(-1)
     return torch.searchsorted(bin_lin[:n_agents].to(torch.int64), targets).to(torch.int32)
-
-
-EX_ROWS, EX_LEVELS, EX_CAP = 64, 3, 1152      # vk_stencil_ps.h: the exchange image's region rows, levels, LDS slots
-EX_TILE_W, EX_HALO = 96, 16                   # variant 70's written columns and halo columns per side
-
-
-class ExchangeImage:
-    """The agent layout of vk_diffuse_exchange's image (see :func:`exchange_image`)."""
-
-    def __init__(self, inv, xhdr, xoff, xbad, ximg, tiles, rows):
-        self.inv, self.xhdr, self.xoff, self.xbad, self.ximg = inv, xhdr, xoff, xbad, ximg
-        self.tiles, self.rows = tiles, rows
-
-
-def exchange_image(bin_lin: torch.Tensor, n_agents: int, rows: int, ny: int, n_fields: int,
-                   chunk_rows: int = EX_ROWS) -> ExchangeImage:
-    """The static part of the exchange image the final pass of vk_diffuse_exchange
-    reads (include/vk_kinetics.h): the agents (stored in bin order) grouped by the
-    pass's wave regions -- ``chunk_rows`` rows x one 96-column tile of variant 70 --
-    in bin order within a region; per region row the lane masks of its agents, which
-    of a lane's two cells each one is in, and its first entry.  A region whose rows
-    hold more than four agents in one lane's cells or more than 64 agents, or more
-    agents than the pass's LDS slots, is marked to add its exchange after its stores.
-    Rebuilt whenever the agent layout changes (Colony._update_coupling)."""
-    dev = bin_lin.device
-    n = int(n_agents)
-    tiles = (ny + EX_TILE_W - 1) // EX_TILE_W
-    chunks = (rows + chunk_rows - 1) // chunk_rows
-    regions = tiles * chunks
-    i64 = torch.int64
-    b = bin_lin[:n].to(i64)
-    r, c = b // ny, b % ny
-    tx, ty = c // EX_TILE_W, r // chunk_rows
-    region = ty * tiles + tx
-    colt = c - tx * EX_TILE_W + EX_HALO                  # the column in the tile: lane = colt // 2
-    order = torch.sort(region, stable=True).indices     # bin order within a region (agents are in bin order)
-    per = torch.bincount(region, minlength=regions)
-    # each region starts at a 16-B multiple of the image (the pass copies it by 16-B LDS-DMA)
-    xoff = torch.zeros(regions + 1, dtype=i64, device=dev)
-    xoff[1:] = torch.cumsum((per + 1) // 2 * 2, 0)
-    reg_s = region[order]
-    first = torch.zeros(regions + 1, dtype=i64, device=dev)
-    first[1:] = torch.cumsum(per, 0)
-    slot = xoff[reg_s] + torch.arange(n, dtype=i64, device=dev) - first[reg_s]
-    inv = torch.full((int(xoff[-1]),), -1, dtype=torch.int32, device=dev)    # entry -> agent (-1: padding)
-    inv[slot] = order.to(torch.int32)
-    rowkey = reg_s * chunk_rows + (r - ty * chunk_rows)[order]
-    lane_s = (colt // 2)[order]
-    q_s = (colt % 2)[order]
-    idx = torch.arange(n, dtype=i64, device=dev)
-    k = idx - first[reg_s]                               # entry within the region
-    nrow = regions * chunk_rows
-    e0 = torch.zeros(nrow, dtype=i64, device=dev)
-    if n:
-        e0.scatter_reduce_(0, rowkey, k, reduce='amin', include_self=False)
-    kr = k - e0[rowkey]                                  # entry within the row
-    key = rowkey * 64 + lane_s
-    start = torch.ones(n, dtype=torch.bool, device=dev)
-    if n > 1:
-        start[1:] = key[1:] != key[:-1]
-    level = idx - torch.cummax(torch.where(start, idx, torch.zeros_like(idx)), 0).values
-    bad = torch.zeros(regions, dtype=torch.bool, device=dev)
-    over = (level >= EX_LEVELS) | (kr >= 64)
-    if bool(over.any()):
-        bad[reg_s[over]] = True
-    bad |= per > EX_CAP
-    hdr = torch.zeros((nrow, 6), dtype=i64, device=dev)
-    one = torch.ones(n, dtype=i64, device=dev)
-    for j in range(EX_LEVELS):
-        sel = level == j
-        hdr[:, j].scatter_add_(0, rowkey[sel], one[sel] << lane_s[sel])
-    sel = (q_s == 1) & (kr < 64)
-    hdr[:, 4].scatter_add_(0, rowkey[sel], one[sel] << kr[sel])
-    hdr[:, 5] = e0
-    # each plane's row of entries with 1 KB of slack (the pass copies whole 1-KB pieces)
-    ximg = torch.zeros((n_fields, int(xoff[-1]) + 128), dtype=torch.float64, device=dev)
-    return ExchangeImage(inv, hdr.contiguous(), xoff.to(torch.int32), bad.to(torch.uint8), ximg, tiles, chunk_rows)
 
 
 def occupancy(bin_lin: torch.Tensor, n_agents: int, order_key: Optional[torch.Tensor] = None):

@@ -27,7 +27,7 @@ VK_AGENT_MAX_STEPS, VK_AGENT_H_UNDERFLOW, VK_AGENT_NONFINITE = 1, 2, 4
 EXPORTS = (
     'vk_abi_version', 'vk_last_error', 'vk_table_create', 'vk_table_destroy', 'vk_table_specialize',
     'vk_rate_fluxes', 'vk_step_euler', 'vk_step_dopri5', 'vk_step_dopri5_multi', 'vk_step_dopri5_gather', 'vk_field_uniform',
-    'vk_diffuse', 'vk_diffuse_part', 'vk_diffuse_delta', 'vk_diffuse_coupled', 'vk_diffuse_exchange', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_set_stencil_mode',
+    'vk_diffuse', 'vk_diffuse_part', 'vk_diffuse_delta', 'vk_diffuse_coupled', 'vk_set_stencil_depth', 'vk_set_stencil_kernel', 'vk_set_stencil_mode',
     'vk_timestamp', 'vk_wall_clock_khz', 'vk_copy_stream', 'vk_gather', 'vk_exchange_sorted',
     'vk_exchange_atomic', 'vk_bin_sites', 'vk_cell_step', 'vk_divide_scratch_bytes', 'vk_divide_plan',
     'vk_divide_gather', 'vk_divide_lineage', 'vk_divide_locations', 'vk_kremling_step',
@@ -109,8 +109,6 @@ _SIGS = {
                           _i32, _i32, _i32, _f64, _vp, _vp], ctypes.c_int),
     'vk_diffuse_coupled': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _f64, _vp, _vp, _vp, _i32, _i64,
                             _i32p, _vp, _i64, _i32p, _vp, _i64, _f64, _vp], ctypes.c_int),
-    'vk_diffuse_exchange': ([_vp, _vp, _vp, _i32, _i64, _i32, _i32, _i32, _f64, _vp, _vp, _vp, _i32, _i64,
-                             _i32p, _vp, _i64, _f64, _vp, _vp, _vp, _vp, _vp, _i64, _i32, _i32, _vp], ctypes.c_int),
     'vk_set_stencil_depth': ([_i32], ctypes.c_int),
     'vk_set_stencil_kernel': ([_i32, _i32], ctypes.c_int),
     'vk_set_stencil_mode': ([_i32], ctypes.c_int),

@@ -28,18 +28,18 @@ def test_stencil_kernel_names_follow_the_launch_rules():
     streams its stores, a 10-deep pass of <= 192 MiB (C3's 1024^2 x 2) stores
     through the caches (vk_stencil_ps10.hip), variant 40 is the stage-split pass."""
     whole = 16 * 4096 * 4096 * 2
-    assert bench.stencil_kernel_name(20, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0, 0, false>'
-    assert bench.stencil_kernel_name(20, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, 0, false>'
-    assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0, false>'
+    assert bench.stencil_kernel_name(20, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0, 0>'
+    assert bench.stencil_kernel_name(20, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, 0>'
+    assert bench.stencil_kernel_name(20, 9, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0>'
     assert bench.stencil_kernel_name(40, 10, 'fma', whole) == 'vk_sp::k_diffuse_sp<10, 4, 2, 5, true, 0>'
-    assert bench.stencil_kernel_name(70, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0, 16, false>'
-    assert bench.stencil_kernel_name(70, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, 16, false>'
-    assert bench.stencil_kernel_name(70, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0, false>'
-    assert bench.stencil_kernel_name(40, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0, false>'
+    assert bench.stencil_kernel_name(70, 10, 'fma', whole) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 0, 16>'
+    assert bench.stencil_kernel_name(70, 10, 'fma', 16 * 1024 * 1024 * 2) == 'vk_ps::k_diffuse_ps<10, 4, 2, true, 2, 16>'
+    assert bench.stencil_kernel_name(70, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0>'
+    assert bench.stencil_kernel_name(40, 9, 'fma', whole) == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0>'
     assert bench.stencil_kernel_name(6, 9, 'exact') == 'vk_nt::k_diffuse_wl<9, 6, false>'
     assert bench.stencil_kernel_name(6, 10, 'exact') == 'vk_nt::k_diffuse_wl<10, 3, false>'
     # the tolerance mode's wave-tile FMA form is retired: variant 6 selects the pair-sum pass
-    assert bench.stencil_kernel_name(6, 9, 'fma') == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0, false>'
+    assert bench.stencil_kernel_name(6, 9, 'fma') == 'vk_ps::k_diffuse_ps<9, 4, 2, true, 0, 0>'
     assert bench.stencil_kernel_name(20, 13, 'fma') == 'vk_nt::k_diffuse_wl<13, 6, false>'.replace('vk_nt::', '')
 
 

@@ -77,7 +77,6 @@ def _pair(dev, nx, ny, n, crowd=0, seed=3, integrator='euler'):
         col.gather_external()
         col.sort_by_bin()
         col.fuse_coupling = fused
-        col.exchange_in_pass = False      # the separate launches (tests/test_exchange_in_pass.py: the store path)
         out.append((col, lat))
     return out
 
@@ -180,7 +179,6 @@ def test_c4_coupled_step_equals_separate_launches(dev):
         del a
         b = bench.build_rank(args, 0, 1, dev)[:2]
         b[0].fuse_coupling = False
-        b[0].exchange_in_pass = False
         b[0].step(1.0)
         torch.cuda.synchronize()
         for f, m in zip(fa, b[1].molecules):
