@@ -407,11 +407,11 @@ constexpr double SAFETY = 0.9, MIN_FACTOR = 0.2, MAX_FACTOR = 10.0;
 // 8a), not bit-parity, so they use the cheap forms of their two costliest
 // operations; the specialised kernel (vk_dopri5_spec.hip.in) uses the same
 // two, so it stays bit-identical to the table walk.
-// a/b by the hardware reciprocal plus two Newton steps (within an ulp or so;
+// a/b by the hardware reciprocal plus one Newton step (~1e-15 relative, as
+// vk_kremling.hip's; a second step bought nothing the 1e-6 odeint bar sees;
 // a zero divisor gives NaN instead of inf -- flagged non-finite either way).
 __device__ __forceinline__ double fdiv(double a, double b) {
     double r = __builtin_amdgcn_rcp(b);
-    r = fma(fma(-b, r, 1.0), r, r);
     r = fma(fma(-b, r, 1.0), r, r);
     return a * r;
 }
