@@ -202,13 +202,15 @@ def split_layout(t: RateLawTable):
     return lanes, dst, second, sets
 
 
-def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int = 0, split_den: int = 0) -> str:
+def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int = 0, split_den: int = 0,
+                group: int = 2) -> str:
     """Complete HIP source of the specialised agent-per-wavefront kernel ``vk_dopri5_wspec``.
 
     split_den = 1 lays the rate laws out two lanes per heavy denominator
     (:func:`split_layout`): the padded denominator shape shrinks (C5: 6 sets x 3
     members -> 4 x 3) and the kernel fits three waves per SIMD; the sum is the
-    table walk's, so results stay bit-identical."""
+    table walk's, so results stay bit-identical.  group = agents (waves) per
+    workgroup; the launcher reads it back from the kernel's launch bound."""
     sh = wave_shape(t)
     W = WAVE_LANES
     ns, nr, nl, nd = t.n_species, t.n_reactions, t.n_rate_laws, t.n_dyn
@@ -277,7 +279,8 @@ def wave_source(t: RateLawTable, wpe: int = 3, pad_writes: int = 0, lds_ops: int
         ('NS', ns), ('ND', nd), ('NR', nr), ('NL', nl), ('NY', ny), ('LR', LR), ('SN', SN), ('MN', MN),
         ('SD', SD), ('MD', MD), ('NSLOT', NSLOT), ('UM', UM), ('RX_IDENTITY', sh['RX_IDENTITY']),
         ('RXR', RXR), ('RXM', RXM), ('TILE', ns + 1 + nr + 1 + nl + 1 + (W if pad_writes else 0)), ('WPE', wpe),
-        ('PAD_WRITES', int(pad_writes)), ('LDS_OPS', int(lds_ops)), ('SPLIT_DEN', int(lay is not None)), ('SB', SB)])
+        ('PAD_WRITES', int(pad_writes)), ('LDS_OPS', int(lds_ops)), ('SPLIT_DEN', int(lay is not None)), ('SB', SB),
+        ('DW_WAVES', int(group))])
     umk = [max([int(t.upd_ptr[i + 1] - t.upd_ptr[i]) for i in range(k * W, min(nd, (k + 1) * W))] or [0])
            for k in range(NSLOT)]
     defs += '\n__device__ constexpr int UMK[NSLOT] = {%s};' % ', '.join(str(u) for u in umk)

@@ -31,6 +31,7 @@ struct vk_table {
     hipModule_t spec_module = nullptr;     // vk_table_specialize (hiprtc)
     hipFunction_t spec_dopri5 = nullptr;      // agent per lane (variant 2)
     hipFunction_t spec_wave = nullptr;        // agent per wavefront (variant 3)
+    int spec_wave_waves = 4;                  // its waves (agents) per workgroup: the launch bound / 64
     hipFunction_t spec_multi = nullptr;       // agent per lane, several steps per launch (vk_step_dopri5_multi)
     hipFunction_t spec_gather = nullptr;      // agent per lane + the next step's gather (vk_step_dopri5_gather)
 };

@@ -223,6 +223,14 @@ extern "C" int vk_table_specialize(vk_table *t, const char *source) {
     t->spec_module = mod;
     t->spec_dopri5 = fn;
     t->spec_wave = fw;
+    t->spec_wave_waves = 4;
+    if (fw) {   // the template's __launch_bounds__(64 * DW_WAVES) says how many agents a workgroup takes
+        int mt = 0;
+        if (hipFuncGetAttribute(&mt, HIP_FUNC_ATTRIBUTE_MAX_THREADS_PER_BLOCK, fw) == hipSuccess && mt >= 64 &&
+            mt % 64 == 0)
+            t->spec_wave_waves = mt / 64;
+        (void)hipGetLastError();
+    }
     t->spec_multi = fm;
     t->spec_gather = fg;
     return VK_OK;
@@ -1139,8 +1147,9 @@ extern "C" int vk_step_dopri5(const vk_table *t, int64_t n, int64_t ld, double d
         int max_steps = o->max_steps;
         void *args[] = {&n, &ld, &dt, &rtol, &atol, &max_steps, (void *)&params, &conc, (void *)&m2c,
                         &delta, &h_state, &flux, &counts, &status, &nsteps};
-        const unsigned blocks = (unsigned)((n + DW_WAVES - 1) / DW_WAVES);
-        return vk::hip_check(hipModuleLaunchKernel(t->spec_wave, blocks, 1, 1, DW * DW_WAVES, 1, 1, 0,
+        const int wg = t->spec_wave_waves;
+        const unsigned blocks = (unsigned)((n + wg - 1) / wg);
+        return vk::hip_check(hipModuleLaunchKernel(t->spec_wave, blocks, 1, 1, DW * wg, 1, 1, 0,
                                                    (hipStream_t)stream, args, nullptr),
                              "hipModuleLaunchKernel(vk_dopri5_wspec)");
     }

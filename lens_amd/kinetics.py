@@ -8,6 +8,7 @@ Thin, shape-checked wrappers over the C ABI.  Layout (``include/vk_kinetics.h``)
 
 from __future__ import annotations
 
+import os
 import ctypes
 
 import torch
@@ -57,7 +58,8 @@ class KineticsEngine:
             # 3 waves per SIMD where the split layout's estimate leaves room (C5: 162 -> 167
             # VGPRs, 16 spilled, 0.63 VALU busy); larger networks keep 2
             wpe = self.WAVE_WAVES_PER_SIMD or (3 if split and wave_registers(self.table, True) <= 165 else 2)
-            src = wave_source(self.table, wpe, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS, split)
+            src = wave_source(self.table, wpe, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS, split,
+                              int(os.environ.get('VK_WAVE_GROUP', self.WAVE_GROUP)))
         else:
             src = dopri5_source(self.table)
         with torch.cuda.device(self.device):
@@ -77,6 +79,10 @@ class KineticsEngine:
     WAVE_SPLIT_DEN = 1          # 1: the heaviest denominators split over lanes l and l + 32 (codegen.split_layout),
                                 # summed in set order (bit-identical); C5 112.0 -> 87.3 ms at 3 waves/SIMD
                                 # (profiles/r03/r03i_c5_probe.log)
+    WAVE_GROUP = 2              # agents (waves) per workgroup of the specialised wavefront kernel: a
+                                # workgroup's slots free only together, and an agent's attempt count
+                                # varies 2x across a colony; C5 kinetics 37.5 ms at 4, 30.9 at 2,
+                                # 30.9-31.1 at 1 (profiles/r06/c5grp; env VK_WAVE_GROUP overrides)
     WAVE_WAVES_PER_SIMD = None  # occupancy the specialised wavefront kernel is compiled for; None: 3 with split
                                 # denominators (190 -> 167 VGPRs, 16 spilled), else 2 (the batched gathers need
                                 # 216 VGPRs; C5: 2 waves 120.5 ms, 3 waves spill, 224 ms)
