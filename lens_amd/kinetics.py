@@ -57,7 +57,8 @@ class KineticsEngine:
             split = int(bool(self.WAVE_SPLIT_DEN) and split_layout(self.table) is not None)
             # 3 waves per SIMD where the split layout's estimate leaves room (C5: 162 -> 167
             # VGPRs, 16 spilled, 0.63 VALU busy); larger networks keep 2
-            wpe = self.WAVE_WAVES_PER_SIMD or (3 if split and wave_registers(self.table, True) <= 165 else 2)
+            wpe = int(os.environ.get('VK_WAVE_WPE', 0)) or self.WAVE_WAVES_PER_SIMD or \
+                (3 if split and wave_registers(self.table, True) <= 165 else 2)
             src = wave_source(self.table, wpe, self.WAVE_PAD_WRITES, self.WAVE_LDS_OPS, split,
                               int(os.environ.get('VK_WAVE_GROUP', self.WAVE_GROUP)))
         else:
@@ -83,7 +84,9 @@ class KineticsEngine:
                                 # workgroup's slots free only together, and an agent's attempt count
                                 # varies 2x across a colony; C5 kinetics 37.5 ms at 4, 30.9 at 2,
                                 # 30.9-31.1 at 1 (profiles/r06/c5grp; env VK_WAVE_GROUP overrides)
-    WAVE_WAVES_PER_SIMD = None  # occupancy the specialised wavefront kernel is compiled for; None: 3 with split
+    WAVE_WAVES_PER_SIMD = None  # occupancy the specialised wavefront kernel is compiled for (env VK_WAVE_WPE
+                                # overrides; with 2-agent workgroups 2 and 3 tie, 4 spills: profiles/r06/c5wpe);
+                                # None: 3 with split
                                 # denominators (190 -> 167 VGPRs, 16 spilled), else 2 (the batched gathers need
                                 # 216 VGPRs; C5: 2 waves 120.5 ms, 3 waves spill, 224 ms)
 
