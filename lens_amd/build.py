@@ -27,6 +27,13 @@ COMPILE = [
     '-Wall', '-Wno-unused-function',
     '-I' + os.path.join(REPO, 'include'), '-I' + os.path.join(HERE, 'csrc'),
 ]
+# Per-unit extra flags.  The pair-sum passes keep v_fma_f64 (three-address) instead of
+# v_fmac_f64 (same bits): the accumulator-tied fmac forced 30 register copies per 6 rows
+# of the 10-deep steady loop (642 -> 612 VALU instructions, same VGPRs; C4 1.255-1.263
+# -> 1.240-1.250 ms per step, profiles/r06/nofmac).  Kremling sheds 458 copies the same
+# way but runs no faster (r06/kremab), so it keeps the default
+EXTRA = {name: ['-Xclang', '-target-feature', '-Xclang', '-fmacf64-inst']
+         for name in ('vk_stencil_ps.hip', 'vk_stencil_ps10.hip', 'vk_stencil_sp.hip')}
 LINK = ['--offload-arch=' + ARCH, '-shared', '-fPIC', '-Wl,--no-undefined', '-Wl,-rpath,/opt/rocm/lib', '-lhiprtc']
 OBJ_DIR = os.path.join(HERE, 'lib', 'obj')
 
@@ -49,7 +56,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         jobs = max(1, min(len(todo), int(os.environ.get('MAX_JOBS', '0')) or (os.cpu_count() or 1)))
 
         def compile_one(pair):
-            cmd = [HIPCC] + COMPILE + ['-c', pair[0], '-o', pair[1] + '.tmp']
+            cmd = [HIPCC] + COMPILE + EXTRA.get(os.path.basename(pair[0]), []) + ['-c', pair[0], '-o', pair[1] + '.tmp']
             if verbose:
                 print('[lens_amd.build]', ' '.join(cmd), flush=True)
             subprocess.run(cmd, check=True)

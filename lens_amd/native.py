@@ -18,7 +18,7 @@ import os
 import numpy as np
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'lib')
-LIB_PATH = os.path.join(LIB_DIR, 'libvk_kinetics.so')
+LIB_PATH = os.environ.get('VK_KINETICS_LIB') or os.path.join(LIB_DIR, 'libvk_kinetics.so')   # env: A/B builds
 
 VK_OK, VK_ERR_ARG, VK_ERR_HIP, VK_ERR_LIMIT, VK_ERR_NOMEM = 0, 1, 2, 3, 4
 VK_AGENT_MAX_STEPS, VK_AGENT_H_UNDERFLOW, VK_AGENT_NONFINITE = 1, 2, 4
