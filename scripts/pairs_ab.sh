@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Record of a reverted experiment: variant 77 is no longer built; DESIGN §10, profiles/r06/pairs.)
 # Variant 77 (paired, half-rotated chunk order) against variant 70: bitwise tests, the
 # bench A/B (C4 headline leg), and each kernel's FETCH_SIZE / WRITE_SIZE.
 set -o pipefail

@@ -1,5 +1,10 @@
 """Diagnostic (needs a build with VK_PS_STAMPS): per-wave start/end times of the C4
-pass (4096^2 x 2, depth 10, variant 70, 64-row tiles), slot occupancy over time."""
+pass (4096^2 x 2, depth 10, variant 70, 64-row tiles), slot occupancy over time.
+
+The instrumentation was a temporary patch, reverted after the measurement: the
+kernel read s_memrealtime at its start and end, and lane 0 stored {start, end,
+HW_ID, XCC_ID} with vector stores into a device buffer set by vk_ps_set_stamps
+(profiles/r06/stamps)."""
 import os, sys, ctypes, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np

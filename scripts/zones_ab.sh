@@ -1,4 +1,5 @@
 #!/bin/bash
+# (Record of a reverted experiment: the VK_ZONES hook is no longer built; DESIGN §10, profiles/r06/zones.)
 # Zoned chunk heights (VK_ZONES="rows2,pct": the last pct % of rows in rows2-row tiles,
 # dispatched last) against one zone: bitwise check, wave stamps, bench arms.
 set -o pipefail
